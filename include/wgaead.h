@@ -1,0 +1,173 @@
+/*
+ * wgaead.h — C-ABI of libwgaead.so, the MI355X (gfx950) transport-data AEAD.
+ *
+ * This is the drop-in boundary for the reference's ChaCha20-Poly1305 path in
+ * module ax.xz.wireguard.noise. Every entry point below names the reference
+ * interface it replaces (file:line, paths relative to the reference root,
+ * abbreviated: NOISE = ax.xz.wireguard.noise/src/main/java/ax/xz/wireguard/noise).
+ * The Java host binds these through Panama exactly as the reference binds
+ * libchacha / libpoly1305-donna today (NOISE/crypto/ChaCha20.java:14-42,
+ * NOISE/crypto/Poly1305.java:24-77); see INTEGRATION.md.
+ *
+ * Conventions
+ *  - Plain C types only; no exceptions cross the ABI.
+ *  - Every function returns 0 (WG_OK) or a negative WG_E* code. A per-packet
+ *    authentication failure is NOT an error return: it is reported in the
+ *    status array (WG_PKT_BADTAG), mirroring the per-packet
+ *    AEADBadTagException of NOISE/crypto/ChaCha20Poly1305.java:51-53.
+ *  - "batch" calls take DEVICE pointers and are asynchronous on `stream`
+ *    (a hipStream_t passed as void*; NULL = the context's own stream).
+ *    The "host" calls take host pointers and return after completion.
+ *  - Packets are independent (no cross-packet state): a batch shards freely
+ *    across devices; no collective is involved (one wg_ctx per device).
+ *  - Nonce layout of transport packets is the reference's, not the WireGuard
+ *    spec's: nonce = LE64(counter) || 00 00 00 00 (NOISE/handshake/SymmetricKeypair.java:52-61).
+ */
+#ifndef WGAEAD_H
+#define WGAEAD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WG_OK 0
+#define WG_EINVAL (-22)    /* bad argument (NULL, n mismatch, unaligned key slot, ...) */
+#define WG_ENOMEM (-12)    /* device or pinned allocation failed */
+#define WG_ERANGE (-34)    /* key slot / buffer bound exceeded by a descriptor */
+#define WG_E2BIG (-7)      /* packet longer than WG_MAX_PACKET */
+#define WG_EDEVICE (-5)    /* HIP runtime error (message via wg_last_error) */
+#define WG_ESELFTEST (-74) /* known-answer self test failed */
+
+#define WG_PKT_OK 0u
+#define WG_PKT_BADTAG 1u
+
+#define WG_TAG_SIZE 16   /* Crypto.ChaChaPoly1305Overhead (NOISE/crypto/Crypto.java:14) */
+#define WG_NONCE_SIZE 12 /* Crypto.ChaChaPoly1305NonceSize (NOISE/crypto/Crypto.java:13) */
+#define WG_KEY_SIZE 32
+#define WG_MAX_PACKET 65535u /* largest payload one workgroup tile accepts */
+
+/* Transport packet descriptor (32 bytes). One per packet of a batch.
+ *  seal: reads  in[in_off .. in_off+len)            plaintext
+ *        writes out[out_off .. out_off+len+16)     ciphertext || tag
+ *        (SymmetricKeypair.cipher: dst = ct || tag, SymmetricKeypair.java:63-74)
+ *  open: reads  in[in_off .. in_off+len+16)         ciphertext || tag
+ *        writes out[out_off .. out_off+len)         plaintext, only if the tag verifies;
+ *        on a bad tag the plaintext range is zero-filled and status = WG_PKT_BADTAG
+ *        (SymmetricKeypair.decipher: L = src.size - 16, SymmetricKeypair.java:76-83)
+ *  counter: the 64-bit transport counter (TransportPacket.java:53-55); nonce built on device.
+ *  key_slot: index into the context's device key table (wg_keys_set). */
+typedef struct wg_pkt {
+  uint64_t in_off;
+  uint64_t out_off;
+  uint64_t counter;
+  uint32_t len;
+  uint32_t key_slot;
+} wg_pkt;
+
+/* General AEAD / primitive descriptor (64 bytes) for the reference's static
+ * crypto API (ChaCha20Poly1305, ChaCha20, Poly1305 classes): explicit 12-byte
+ * nonce words, optional AAD, explicit initial block counter. */
+typedef struct wg_aead_desc {
+  uint64_t in_off;
+  uint64_t out_off;
+  uint64_t aad_off;   /* into the aad buffer (AEAD modes only) */
+  uint32_t len;       /* payload bytes (excl. tag) */
+  uint32_t aad_len;   /* 0 = no AAD (poly1305AeadEncrypt(key, nonce, ...) overloads) */
+  uint32_t key_slot;  /* ChaCha key (AEAD, CIPHER) or 32-byte one-time key (MAC) */
+  uint32_t ctr0;      /* CIPHER mode: initial 32-bit block counter (ChaCha20.chacha20(..., counter)) */
+  uint32_t nonce[3];  /* state words 13..15, little-endian (ChaCha20.java:265) */
+  uint32_t _reserved[3];
+} wg_aead_desc;
+
+typedef struct wg_ctx wg_ctx;
+
+/* ---- library / context -------------------------------------------------- */
+
+/* Known-answer self test on the device (RFC 8439 2.3.2/2.4.2/2.5.2/2.6.2/2.8.2
+ * and the donna vectors). Returns 1 if all pass, like poly1305_power_on_self_test
+ * which Poly1305.<clinit> checks (Poly1305.java:62-76). Creates and destroys a
+ * temporary context on `device`. */
+int wg_aead_selftest(int device);
+
+/* Create a context bound to HIP device `device` with a key table of
+ * `key_slots` 32-byte entries (zero-initialised). */
+int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out);
+int wg_ctx_destroy(wg_ctx* ctx); /* zeroes the key table first */
+int wg_ctx_device(const wg_ctx* ctx);
+uint32_t wg_ctx_key_slots(const wg_ctx* ctx);
+void* wg_ctx_stream(wg_ctx* ctx);       /* the context's hipStream_t */
+int wg_sync(wg_ctx* ctx, void* stream); /* hipStreamSynchronize */
+const char* wg_last_error(void);        /* thread-local text for the last error */
+const char* wg_version(void);
+
+/* ---- keys: SymmetricKeypair(byte[] send, byte[] recv) and clean() ---------
+ * (SymmetricKeypair.java:39-50 copies keys into a shared Arena; :85-93 zeroes them) */
+int wg_keys_set(wg_ctx* ctx, uint32_t first_slot, uint32_t n, const uint8_t* keys_host /* n*32 */);
+int wg_keys_zero(wg_ctx* ctx, uint32_t first_slot, uint32_t n);
+
+/* ---- batched transport seal / open (device pointers) ----------------------
+ * Replaces the per-packet ForkJoinPool fan-out of SymmetricKeypair.cipher /
+ * decipher (TransportManager.java:41,70-93,137-158). `in_size` / `out_size`
+ * are the byte sizes of the buffers; every descriptor is bounds-checked on
+ * device against them (an out-of-range packet is skipped with status
+ * WG_PKT_BADTAG on open / untouched output on seal, and the call returns 0).
+ * `max_len`: every packet's len must be <= max_len (longer ones are treated
+ * as out of range); it sizes the LDS tile. Flags: WG_F_UNIFORM promises every
+ * desc[i].len == max_len (closed-form tile plan, no device scan); without it
+ * the tile plan is built on device (block-count scan). */
+#define WG_F_UNIFORM 1u
+int wg_seal_batch(wg_ctx* ctx, const wg_pkt* desc_dev, uint32_t n, const uint8_t* in_dev, uint64_t in_size,
+                  uint8_t* out_dev, uint64_t out_size, uint32_t max_len, uint32_t flags, void* stream);
+int wg_open_batch(wg_ctx* ctx, const wg_pkt* desc_dev, uint32_t n, const uint8_t* in_dev, uint64_t in_size,
+                  uint8_t* out_dev, uint64_t out_size, uint32_t* status_dev, uint32_t max_len, uint32_t flags,
+                  void* stream);
+
+/* ---- general AEAD + primitives (device pointers) --------------------------
+ * WG_MODE_SEAL / WG_MODE_OPEN: ChaCha20Poly1305.poly1305AeadEncrypt / Decrypt
+ *   with optional AAD and explicit nonce (ChaCha20Poly1305.java:31-60).
+ * WG_MODE_CIPHER: ChaCha20.chacha20(key, nonce, in, out, counter) (ChaCha20.java:116-131)
+ *   = libchacha chacha_cipher with state word 12 = ctr0 (chacha-generic.c:104-108).
+ * WG_MODE_MAC: Poly1305 init/update/finish one-shot with a 32-byte one-time key
+ *   (Poly1305.java:94-166 over poly1305-donna.c:26-69); tag at out[out_off]. */
+#define WG_MODE_SEAL 0
+#define WG_MODE_OPEN 1
+#define WG_MODE_CIPHER 2
+#define WG_MODE_MAC 3
+int wg_aead_batch(wg_ctx* ctx, int mode, const wg_aead_desc* desc_dev, uint32_t n, const uint8_t* in_dev,
+                  uint64_t in_size, const uint8_t* aad_dev, uint64_t aad_size, uint8_t* out_dev, uint64_t out_size,
+                  uint32_t* status_dev, uint32_t max_len, void* stream);
+
+/* ---- host-buffer entry points (synchronous; stage through pinned memory) --
+ * wg_seal1 / wg_open1 back the unchanged per-packet SymmetricKeypair API:
+ *   cipher(src, dst): wg_seal1(ctx, send_slot, counter, src, L, dst) with dst of L+16 bytes
+ *   decipher(counter, src, dst): wg_open1(ctx, recv_slot, counter, src, L, dst) with src of L+16 bytes
+ *   returns WG_OK, or 1 for a bad tag (dst untouched, as NOISE/crypto/ChaCha20Poly1305.java:51-55).
+ * wg_seal_host / wg_open_host: a batch in host memory (tun ring in, UDP ring out),
+ *   pipelined H2D -> kernel -> D2H in chunks over two streams. */
+int wg_seal1(wg_ctx* ctx, uint32_t key_slot, uint64_t counter, const uint8_t* pt, uint32_t len, uint8_t* out);
+int wg_open1(wg_ctx* ctx, uint32_t key_slot, uint64_t counter, const uint8_t* in, uint32_t len, uint8_t* pt);
+int wg_seal_host(wg_ctx* ctx, const wg_pkt* desc_host, uint32_t n, const uint8_t* in_host, uint64_t in_size,
+                 uint8_t* out_host, uint64_t out_size, uint32_t max_len, uint32_t flags);
+int wg_open_host(wg_ctx* ctx, const wg_pkt* desc_host, uint32_t n, const uint8_t* in_host, uint64_t in_size,
+                 uint8_t* out_host, uint64_t out_size, uint32_t* status_host, uint32_t max_len, uint32_t flags);
+/* General AEAD / primitives on host buffers with a per-call key list
+ * (desc[i].key_slot indexes keys_host[nkeys][32]); the device copy of the keys
+ * is zeroed before returning. */
+int wg_aead_host(wg_ctx* ctx, int mode, const wg_aead_desc* desc_host, uint32_t n, const uint8_t* keys_host,
+                 uint32_t nkeys, const uint8_t* in_host, uint64_t in_size, const uint8_t* aad_host, uint64_t aad_size,
+                 uint8_t* out_host, uint64_t out_size, uint32_t* status_host);
+
+/* ---- instrumentation -------------------------------------------------------
+ * Average duration (ms) of the last `wg_timing_launches` kernel launches made
+ * by batch calls on this context, measured with HIP events on the launch
+ * stream (used by bench.py for the roofline `achieved` figure). */
+int wg_timing_enable(wg_ctx* ctx, int on);
+int wg_timing_read(wg_ctx* ctx, double* total_ms, uint64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WGAEAD_H */

@@ -1,0 +1,114 @@
+"""ctypes binding of libwgaead.so — the C-ABI declared in include/wgaead.h.
+
+The product path has no CPU fallback: if the shared library (built in-tree by
+``make -C wireguard-java_amd/csrc``) is missing or no HIP device is usable, the
+calls below raise ``WgError`` instead of computing anything on the host.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libwgaead.so")
+
+WG_OK = 0
+WG_EINVAL = -22
+WG_ENOMEM = -12
+WG_ERANGE = -34
+WG_E2BIG = -7
+WG_EDEVICE = -5
+WG_ESELFTEST = -74
+WG_PKT_OK = 0
+WG_PKT_BADTAG = 1
+WG_TAG_SIZE = 16
+WG_NONCE_SIZE = 12
+WG_KEY_SIZE = 32
+WG_MAX_PACKET = 65535
+WG_F_UNIFORM = 1
+WG_MODE_SEAL, WG_MODE_OPEN, WG_MODE_CIPHER, WG_MODE_MAC = 0, 1, 2, 3
+
+_ERRNAMES = {WG_EINVAL: "EINVAL", WG_ENOMEM: "ENOMEM", WG_ERANGE: "ERANGE", WG_E2BIG: "E2BIG",
+             WG_EDEVICE: "EDEVICE", WG_ESELFTEST: "ESELFTEST"}
+
+
+class WgError(RuntimeError):
+    """A negative return code of libwgaead (mirrors the RuntimeException the reference's
+    FFM wrappers raise on a failed downcall, ChaCha20.java:293-295)."""
+
+    def __init__(self, code: int, msg: str = ""):
+        super().__init__(f"libwgaead {_ERRNAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class WgPkt(ctypes.Structure):
+    _fields_ = [("in_off", ctypes.c_uint64), ("out_off", ctypes.c_uint64), ("counter", ctypes.c_uint64),
+                ("len", ctypes.c_uint32), ("key_slot", ctypes.c_uint32)]
+
+
+class WgAeadDesc(ctypes.Structure):
+    _fields_ = [("in_off", ctypes.c_uint64), ("out_off", ctypes.c_uint64), ("aad_off", ctypes.c_uint64),
+                ("len", ctypes.c_uint32), ("aad_len", ctypes.c_uint32), ("key_slot", ctypes.c_uint32),
+                ("ctr0", ctypes.c_uint32), ("nonce", ctypes.c_uint32 * 3), ("_reserved", ctypes.c_uint32 * 3)]
+
+
+assert ctypes.sizeof(WgPkt) == 32 and ctypes.sizeof(WgAeadDesc) == 64
+
+# (name, restype, argtypes) for every symbol include/wgaead.h declares
+_VP, _U32, _U64, _I, _D = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_double
+SIGNATURES = [
+    ("wg_aead_selftest", _I, [_I]),
+    ("wg_ctx_create", _I, [_I, _U32, ctypes.POINTER(_VP)]),
+    ("wg_ctx_destroy", _I, [_VP]),
+    ("wg_ctx_device", _I, [_VP]),
+    ("wg_ctx_key_slots", _U32, [_VP]),
+    ("wg_ctx_stream", _VP, [_VP]),
+    ("wg_sync", _I, [_VP, _VP]),
+    ("wg_last_error", ctypes.c_char_p, []),
+    ("wg_version", ctypes.c_char_p, []),
+    ("wg_keys_set", _I, [_VP, _U32, _U32, _VP]),
+    ("wg_keys_zero", _I, [_VP, _U32, _U32]),
+    ("wg_seal_batch", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _U32, _U32, _VP]),
+    ("wg_open_batch", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _VP, _U32, _U32, _VP]),
+    ("wg_aead_batch", _I, [_VP, _I, _VP, _U32, _VP, _U64, _VP, _U64, _VP, _U64, _VP, _U32, _VP]),
+    ("wg_seal1", _I, [_VP, _U32, _U64, _VP, _U32, _VP]),
+    ("wg_open1", _I, [_VP, _U32, _U64, _VP, _U32, _VP]),
+    ("wg_seal_host", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _U32, _U32]),
+    ("wg_open_host", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _VP, _U32, _U32]),
+    ("wg_aead_host", _I, [_VP, _I, _VP, _U32, _VP, _U32, _VP, _U64, _VP, _U64, _VP, _U64, _VP]),
+    ("wg_timing_enable", _I, [_VP, _I]),
+    ("wg_timing_read", _I, [_VP, ctypes.POINTER(_D), ctypes.POINTER(_U64)]),
+]
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib() -> ctypes.CDLL:
+    """Load libwgaead.so (once). Raises WgError(EDEVICE) when it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise WgError(WG_EDEVICE, f"{LIB_PATH} not built (run `make -C wireguard-java_amd/csrc`)")
+            L = ctypes.CDLL(LIB_PATH)
+            for name, res, args in SIGNATURES:
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    msg = lib().wg_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int) -> int:
+    if rc < 0:
+        raise WgError(rc, last_error())
+    return rc

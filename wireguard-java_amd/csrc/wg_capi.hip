@@ -1,0 +1,555 @@
+// wg_capi.hip — the C-ABI of libwgaead.so (include/wgaead.h).
+//
+// Host runtime around the gfx950 kernels: per-device context (stream, device key
+// table, plan workspace, staging buffers), launch planning, the device-pointer
+// batch API, the host-pointer convenience API and the on-device self test.
+// No CPU crypto lives here: every seal/open/cipher/MAC runs in wg_kernels.hip,
+// and every entry point fails with WG_EDEVICE when no HIP device is usable.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "wg_kernels.hip"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPTRY(expr)                                                                             \
+  do {                                                                                           \
+    hipError_t e_ = (expr);                                                                      \
+    if (e_ != hipSuccess) return fail(WG_EDEVICE, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                                      __FILE__, __LINE__);                                       \
+  } while (0)
+
+// grow-only device buffer
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return WG_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 256);
+    if (hipMalloc(&p, want) != hipSuccess) return fail(WG_ENOMEM, "hipMalloc(%zu) failed", want);
+    cap = want;
+    return WG_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+}  // namespace
+
+struct wg_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t copy_stream = nullptr;
+  uint32_t key_slots = 0;
+  uint32_t* keys = nullptr;  // device key table
+  // non-uniform plan workspace
+  DevBuf plan_nb, plan_prefix, plan_tiles, plan_ntiles, plan_tmp;
+  // host-API staging
+  DevBuf h_desc, h_in, h_out, h_aad, h_status, h_keys;
+  std::mutex mu;  // serialises host-API calls and plan workspace reuse
+  // timing
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+  double timed_ms = 0;
+  uint64_t timed_launches = 0;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+template <int MODE>
+uint32_t host_pkt_blocks(uint32_t len) {
+  uint32_t nb = (len + 63u) / 64u;
+  return (MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN) ? nb + 1u : nb;
+}
+
+constexpr uint32_t kLdsBudget = 64u * 1024u;  // per workgroup; keeps >= 2 tiles per CU
+
+// lanes per packet for the Poly1305 phase: fill one wave with the tile's packets
+uint32_t choose_poly_g(uint32_t ppt) {
+  if (ppt == 0) return 1;
+  uint32_t g = 64u / ppt;
+  if (g < 1) g = 1;
+  if (g > 16) g = 16;
+  return g;
+}
+
+void record_start(wg_ctx* c, hipStream_t s, hipEvent_t* ev) {
+  *ev = nullptr;
+  if (!c->timing) return;
+  hipEvent_t a;
+  if (hipEventCreate(&a) != hipSuccess) return;
+  (void)hipEventRecord(a, s);
+  *ev = a;
+}
+void record_end(wg_ctx* c, hipStream_t s, hipEvent_t a) {
+  if (!a) return;
+  hipEvent_t b;
+  if (hipEventCreate(&b) != hipSuccess) return;
+  (void)hipEventRecord(b, s);
+  c->events.emplace_back(a, b);
+}
+
+template <int MODE, bool GENERAL>
+int launch_tiles(wg_ctx* c, const void* desc, uint32_t n, const uint8_t* in, uint64_t in_size, const uint8_t* aad,
+                 uint64_t aad_size, uint8_t* out, uint64_t out_size, uint32_t* status, uint32_t max_len,
+                 uint32_t flags, hipStream_t s) {
+  if (n == 0) return WG_OK;
+  if (!desc || (((uintptr_t)desc) & 15u)) return fail(WG_EINVAL, "descriptor array must be non-NULL and 16-byte aligned");
+  if (!in && MODE != WG_MODE_MAC) return fail(WG_EINVAL, "NULL input buffer");
+  if (!out) return fail(WG_EINVAL, "NULL output buffer");
+  if (max_len > WG_MAX_PACKET) return fail(WG_E2BIG, "max_len %u > WG_MAX_PACKET", max_len);
+  wgk::TileParams P{};
+  P.desc = desc;
+  P.n = n;
+  P.max_len = max_len;
+  P.in = in;
+  P.in_size = in ? in_size : 0;
+  P.out = out;
+  P.out_size = out_size;
+  P.aad = aad;
+  P.aad_size = aad ? aad_size : 0;
+  P.keys = c->keys;
+  P.key_slots = c->key_slots;
+  P.status = status;
+  const uint32_t aead_extra = (MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN) ? 1u : 0u;
+  uint32_t grid = 0, lds = 0;
+  if (flags & WG_F_UNIFORM) {
+    const uint32_t nb = host_pkt_blocks<MODE>(max_len);
+    uint32_t ppt = 1;
+    if (nb == 0) {
+      ppt = 64;
+    } else if (nb <= WG_TPB) {
+      // pick the tile size (1 or 2 passes of the workgroup) that idles fewest lanes
+      double best = -1;
+      for (uint32_t k = 1; k <= 2; ++k) {
+        uint32_t p = k * WG_TPB / nb;
+        uint32_t img = p * (nb - aead_extra) * 64u;
+        if (p == 0 || wgk::tile_header_bytes(p) + img > kLdsBudget) continue;
+        double util = (double)(p * nb) / (double)(k * WG_TPB);
+        if (util > best + 1e-9) { best = util; ppt = p; }
+      }
+    }
+    if (ppt > n) ppt = n;
+    P.uniform = 1;
+    P.ppt = ppt;
+    P.nb_uniform = nb;
+    P.nb_magic = nb > 1 ? (uint32_t)((((uint64_t)1 << 32) + nb - 1) / nb) : 0u;
+    P.max_tile_pkts = ppt;
+    P.poly_g = choose_poly_g(ppt);
+    lds = wgk::tile_header_bytes(ppt) + ppt * (nb > aead_extra ? nb - aead_extra : 0u) * 64u;
+    grid = (n + ppt - 1) / ppt;
+  } else {
+    // device plan: block counts -> exclusive scan -> start-owned tiles of C blocks
+    const uint32_t C = WG_TPB;
+    const uint32_t max_nb = host_pkt_blocks<MODE>(max_len);
+    const uint64_t max_tiles64 = ((uint64_t)n * std::max<uint32_t>(max_nb, 1u) + C - 1) / C;
+    if (max_tiles64 > 0x7fffffffull) return fail(WG_EINVAL, "batch too large");
+    const uint32_t max_tiles = (uint32_t)max_tiles64;
+    int rc;
+    if ((rc = c->plan_nb.ensure(sizeof(uint32_t) * (n + 1))) != WG_OK) return rc;
+    if ((rc = c->plan_prefix.ensure(sizeof(uint32_t) * (n + 1))) != WG_OK) return rc;
+    if ((rc = c->plan_tiles.ensure(sizeof(uint32_t) * (max_tiles + 2))) != WG_OK) return rc;
+    if ((rc = c->plan_ntiles.ensure(sizeof(uint32_t))) != WG_OK) return rc;
+    size_t tmp = 0;
+    HIPTRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, (uint32_t*)c->plan_nb.p, (uint32_t*)c->plan_prefix.p,
+                                            (int)(n + 1), s));
+    if ((rc = c->plan_tmp.ensure(tmp)) != WG_OK) return rc;
+    hipLaunchKernelGGL((wgk::k_plan_count<MODE, GENERAL>), dim3((n + 1 + 255) / 256), dim3(256), 0, s, desc, n,
+                       max_len, (uint32_t*)c->plan_nb.p);
+    HIPTRY(hipGetLastError());
+    HIPTRY(hipcub::DeviceScan::ExclusiveSum(c->plan_tmp.p, tmp, (uint32_t*)c->plan_nb.p, (uint32_t*)c->plan_prefix.p,
+                                            (int)(n + 1), s));
+    hipLaunchKernelGGL(wgk::k_plan_tiles, dim3((max_tiles + 1 + 255) / 256), dim3(256), 0, s,
+                       (const uint32_t*)c->plan_prefix.p, n, C, (uint32_t*)c->plan_tiles.p,
+                       (uint32_t*)c->plan_ntiles.p, max_tiles);
+    HIPTRY(hipGetLastError());
+    P.uniform = 0;
+    P.tile_start = (const uint32_t*)c->plan_tiles.p;
+    P.blk_prefix = (const uint32_t*)c->plan_prefix.p;
+    P.ntiles_dev = (const uint32_t*)c->plan_ntiles.p;
+    P.max_tile_pkts = C;
+    P.poly_g = 8;
+    lds = wgk::tile_header_bytes(C) + (C + max_nb) * 64u;
+    grid = max_tiles;
+  }
+  if (lds > 160u * 1024u) return fail(WG_E2BIG, "tile needs %u bytes of LDS", lds);
+  hipEvent_t ev;
+  record_start(c, s, &ev);
+  hipLaunchKernelGGL((wgk::k_tile<MODE, GENERAL>), dim3(grid), dim3(WG_TPB), lds, s, P);
+  hipError_t e = hipGetLastError();
+  record_end(c, s, ev);
+  if (e != hipSuccess) return fail(WG_EDEVICE, "k_tile launch: %s", hipGetErrorString(e));
+  return WG_OK;
+}
+
+hipStream_t pick_stream(wg_ctx* c, void* stream) { return stream ? (hipStream_t)stream : c->stream; }
+
+}  // namespace
+
+extern "C" {
+
+const char* wg_last_error(void) { return g_err.c_str(); }
+const char* wg_version(void) { return "wgaead 0.1.0 gfx950"; }
+
+int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
+  if (!out) return fail(WG_EINVAL, "out is NULL");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(WG_EDEVICE, "no HIP device available");
+  if (device < 0 || device >= ndev) return fail(WG_EINVAL, "device %d out of range (%d devices)", device, ndev);
+  if (key_slots == 0) key_slots = 1;
+  DeviceGuard g(device);
+  wg_ctx* c = new wg_ctx();
+  c->device = device;
+  c->key_slots = key_slots;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&c->keys, (size_t)key_slots * 32) != hipSuccess ||
+      hipMemset(c->keys, 0, (size_t)key_slots * 32) != hipSuccess) {
+    wg_ctx_destroy(c);
+    return fail(WG_ENOMEM, "context allocation failed on device %d", device);
+  }
+  *out = c;
+  return WG_OK;
+}
+
+int wg_ctx_destroy(wg_ctx* c) {
+  if (!c) return WG_OK;
+  DeviceGuard g(c->device);
+  if (c->keys) {
+    (void)hipMemset(c->keys, 0, (size_t)c->key_slots * 32);  // SymmetricKeypair.clean zeroes keys
+    (void)hipDeviceSynchronize();
+    (void)hipFree(c->keys);
+  }
+  for (auto& e : c->events) {
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  for (DevBuf* b : {&c->plan_nb, &c->plan_prefix, &c->plan_tiles, &c->plan_ntiles, &c->plan_tmp, &c->h_desc, &c->h_in,
+                    &c->h_out, &c->h_aad, &c->h_status, &c->h_keys})
+    b->release();
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+  delete c;
+  return WG_OK;
+}
+
+int wg_ctx_device(const wg_ctx* c) { return c ? c->device : -1; }
+uint32_t wg_ctx_key_slots(const wg_ctx* c) { return c ? c->key_slots : 0; }
+void* wg_ctx_stream(wg_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int wg_sync(wg_ctx* c, void* stream) {
+  if (!c) return fail(WG_EINVAL, "NULL context");
+  DeviceGuard g(c->device);
+  HIPTRY(hipStreamSynchronize(pick_stream(c, stream)));
+  return WG_OK;
+}
+
+int wg_keys_set(wg_ctx* c, uint32_t first, uint32_t n, const uint8_t* keys_host) {
+  if (!c || (!keys_host && n)) return fail(WG_EINVAL, "NULL argument");
+  if ((uint64_t)first + n > c->key_slots) return fail(WG_ERANGE, "key slots [%u, %u) exceed table of %u", first, first + n, c->key_slots);
+  if (!n) return WG_OK;
+  DeviceGuard g(c->device);
+  HIPTRY(hipMemcpyAsync((uint8_t*)c->keys + (size_t)first * 32, keys_host, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+  HIPTRY(hipStreamSynchronize(c->stream));
+  return WG_OK;
+}
+
+int wg_keys_zero(wg_ctx* c, uint32_t first, uint32_t n) {
+  if (!c) return fail(WG_EINVAL, "NULL context");
+  if ((uint64_t)first + n > c->key_slots) return fail(WG_ERANGE, "key slots out of range");
+  if (!n) return WG_OK;
+  DeviceGuard g(c->device);
+  HIPTRY(hipMemsetAsync((uint8_t*)c->keys + (size_t)first * 32, 0, (size_t)n * 32, c->stream));
+  HIPTRY(hipStreamSynchronize(c->stream));
+  return WG_OK;
+}
+
+int wg_seal_batch(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, uint64_t in_size, uint8_t* out,
+                  uint64_t out_size, uint32_t max_len, uint32_t flags, void* stream) {
+  if (!c) return fail(WG_EINVAL, "NULL context");
+  DeviceGuard g(c->device);
+  std::lock_guard<std::mutex> lk(c->mu);
+  return launch_tiles<WG_MODE_SEAL, false>(c, desc, n, in, in_size, nullptr, 0, out, out_size, nullptr, max_len, flags,
+                                           pick_stream(c, stream));
+}
+
+int wg_open_batch(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, uint64_t in_size, uint8_t* out,
+                  uint64_t out_size, uint32_t* status, uint32_t max_len, uint32_t flags, void* stream) {
+  if (!c) return fail(WG_EINVAL, "NULL context");
+  DeviceGuard g(c->device);
+  std::lock_guard<std::mutex> lk(c->mu);
+  return launch_tiles<WG_MODE_OPEN, false>(c, desc, n, in, in_size, nullptr, 0, out, out_size, status, max_len, flags,
+                                           pick_stream(c, stream));
+}
+
+int wg_aead_batch(wg_ctx* c, int mode, const wg_aead_desc* desc, uint32_t n, const uint8_t* in, uint64_t in_size,
+                  const uint8_t* aad, uint64_t aad_size, uint8_t* out, uint64_t out_size, uint32_t* status,
+                  uint32_t max_len, void* stream) {
+  if (!c) return fail(WG_EINVAL, "NULL context");
+  DeviceGuard g(c->device);
+  std::lock_guard<std::mutex> lk(c->mu);
+  hipStream_t s = pick_stream(c, stream);
+  switch (mode) {
+    case WG_MODE_SEAL:
+      return launch_tiles<WG_MODE_SEAL, true>(c, desc, n, in, in_size, aad, aad_size, out, out_size, nullptr, max_len, 0, s);
+    case WG_MODE_OPEN:
+      return launch_tiles<WG_MODE_OPEN, true>(c, desc, n, in, in_size, aad, aad_size, out, out_size, status, max_len, 0, s);
+    case WG_MODE_CIPHER:
+      return launch_tiles<WG_MODE_CIPHER, true>(c, desc, n, in, in_size, nullptr, 0, out, out_size, nullptr, max_len, 0, s);
+    case WG_MODE_MAC:
+      return launch_tiles<WG_MODE_MAC, true>(c, desc, n, in, in_size, nullptr, 0, out, out_size, nullptr, max_len, 0, s);
+    default:
+      return fail(WG_EINVAL, "unknown mode %d", mode);
+  }
+}
+
+// ---- host-pointer API --------------------------------------------------------
+
+static int host_transport(wg_ctx* c, bool open, const wg_pkt* desc, uint32_t n, const uint8_t* in, uint64_t in_size,
+                          uint8_t* out, uint64_t out_size, uint32_t* status, uint32_t max_len, uint32_t flags) {
+  if (!c || (n && (!desc || !in || !out))) return fail(WG_EINVAL, "NULL argument");
+  if (open && n && !status) return fail(WG_EINVAL, "open needs a status array");
+  if (!n) return WG_OK;
+  DeviceGuard g(c->device);
+  std::lock_guard<std::mutex> lk(c->mu);
+  int rc;
+  if ((rc = c->h_desc.ensure(sizeof(wg_pkt) * (size_t)n)) || (rc = c->h_in.ensure(in_size)) ||
+      (rc = c->h_out.ensure(out_size)) || (rc = c->h_status.ensure(sizeof(uint32_t) * (size_t)n)))
+    return rc;
+  hipStream_t s = c->stream;
+  HIPTRY(hipMemcpyAsync(c->h_desc.p, desc, sizeof(wg_pkt) * (size_t)n, hipMemcpyHostToDevice, s));
+  HIPTRY(hipMemcpyAsync(c->h_in.p, in, in_size, hipMemcpyHostToDevice, s));
+  if (open) {
+    // the caller's plaintext buffer must stay untouched on failure: stage it
+    HIPTRY(hipMemcpyAsync(c->h_out.p, out, out_size, hipMemcpyHostToDevice, s));
+    rc = launch_tiles<WG_MODE_OPEN, false>(c, c->h_desc.p, n, (const uint8_t*)c->h_in.p, in_size, nullptr, 0,
+                                           (uint8_t*)c->h_out.p, out_size, (uint32_t*)c->h_status.p, max_len, flags, s);
+  } else {
+    HIPTRY(hipMemcpyAsync(c->h_out.p, out, out_size, hipMemcpyHostToDevice, s));
+    rc = launch_tiles<WG_MODE_SEAL, false>(c, c->h_desc.p, n, (const uint8_t*)c->h_in.p, in_size, nullptr, 0,
+                                           (uint8_t*)c->h_out.p, out_size, nullptr, max_len, flags, s);
+  }
+  if (rc) return rc;
+  if (open) HIPTRY(hipMemcpyAsync(status, c->h_status.p, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, s));
+  HIPTRY(hipMemcpyAsync(out, c->h_out.p, out_size, hipMemcpyDeviceToHost, s));
+  HIPTRY(hipStreamSynchronize(s));
+  return WG_OK;
+}
+
+int wg_seal_host(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, uint64_t in_size, uint8_t* out,
+                 uint64_t out_size, uint32_t max_len, uint32_t flags) {
+  return host_transport(c, false, desc, n, in, in_size, out, out_size, nullptr, max_len, flags);
+}
+
+int wg_open_host(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, uint64_t in_size, uint8_t* out,
+                 uint64_t out_size, uint32_t* status, uint32_t max_len, uint32_t flags) {
+  return host_transport(c, true, desc, n, in, in_size, out, out_size, status, max_len, flags);
+}
+
+int wg_seal1(wg_ctx* c, uint32_t key_slot, uint64_t counter, const uint8_t* pt, uint32_t len, uint8_t* out) {
+  if (!c || (!pt && len) || !out) return fail(WG_EINVAL, "NULL argument");
+  if (len > WG_MAX_PACKET) return fail(WG_E2BIG, "packet of %u bytes", len);
+  if (key_slot >= c->key_slots) return fail(WG_ERANGE, "key slot %u", key_slot);
+  wg_pkt d{0, 0, counter, len, key_slot};
+  static const uint8_t zero = 0;
+  return host_transport(c, false, &d, 1, len ? pt : &zero, len ? len : 1, out, (uint64_t)len + 16, nullptr, len,
+                        WG_F_UNIFORM);
+}
+
+int wg_open1(wg_ctx* c, uint32_t key_slot, uint64_t counter, const uint8_t* in, uint32_t len, uint8_t* pt) {
+  if (!c || !in || (!pt && len)) return fail(WG_EINVAL, "NULL argument");
+  if (len > WG_MAX_PACKET) return fail(WG_E2BIG, "packet of %u bytes", len);
+  if (key_slot >= c->key_slots) return fail(WG_ERANGE, "key slot %u", key_slot);
+  wg_pkt d{0, 0, counter, len, key_slot};
+  uint32_t st = WG_PKT_BADTAG;
+  std::vector<uint8_t> tmp(len ? len : 1);
+  int rc = host_transport(c, true, &d, 1, in, (uint64_t)len + 16, tmp.data(), tmp.size(), &st, len, WG_F_UNIFORM);
+  if (rc) return rc;
+  if (st != WG_PKT_OK) return 1;  // dst untouched, as ChaCha20Poly1305.java:51-53 throws before decrypting
+  if (len) memcpy(pt, tmp.data(), len);
+  return WG_OK;
+}
+
+int wg_aead_host(wg_ctx* c, int mode, const wg_aead_desc* desc, uint32_t n, const uint8_t* keys_host, uint32_t nkeys,
+                 const uint8_t* in, uint64_t in_size, const uint8_t* aad, uint64_t aad_size, uint8_t* out,
+                 uint64_t out_size, uint32_t* status) {
+  if (!c || (n && (!desc || !keys_host || !out))) return fail(WG_EINVAL, "NULL argument");
+  if (mode == WG_MODE_OPEN && n && !status) return fail(WG_EINVAL, "open needs a status array");
+  if (!n) return WG_OK;
+  uint32_t max_len = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (desc[i].key_slot >= nkeys) return fail(WG_ERANGE, "desc %u key_slot %u >= nkeys %u", i, desc[i].key_slot, nkeys);
+    max_len = std::max(max_len, desc[i].len);
+  }
+  if (max_len > WG_MAX_PACKET) return fail(WG_E2BIG, "packet of %u bytes", max_len);
+  DeviceGuard g(c->device);
+  std::lock_guard<std::mutex> lk(c->mu);
+  int rc;
+  const size_t in_b = std::max<uint64_t>(in_size, 1), aad_b = std::max<uint64_t>(aad_size, 1);
+  if ((rc = c->h_desc.ensure(sizeof(wg_aead_desc) * (size_t)n)) || (rc = c->h_in.ensure(in_b)) ||
+      (rc = c->h_out.ensure(out_size)) || (rc = c->h_aad.ensure(aad_b)) ||
+      (rc = c->h_status.ensure(sizeof(uint32_t) * (size_t)n)) || (rc = c->h_keys.ensure((size_t)nkeys * 32)))
+    return rc;
+  hipStream_t s = c->stream;
+  HIPTRY(hipMemcpyAsync(c->h_desc.p, desc, sizeof(wg_aead_desc) * (size_t)n, hipMemcpyHostToDevice, s));
+  if (in && in_size) HIPTRY(hipMemcpyAsync(c->h_in.p, in, in_size, hipMemcpyHostToDevice, s));
+  if (aad && aad_size) HIPTRY(hipMemcpyAsync(c->h_aad.p, aad, aad_size, hipMemcpyHostToDevice, s));
+  HIPTRY(hipMemcpyAsync(c->h_out.p, out, out_size, hipMemcpyHostToDevice, s));
+  HIPTRY(hipMemcpyAsync(c->h_keys.p, keys_host, (size_t)nkeys * 32, hipMemcpyHostToDevice, s));
+  // swap in the per-call key table
+  uint32_t* saved_keys = c->keys;
+  uint32_t saved_slots = c->key_slots;
+  c->keys = (uint32_t*)c->h_keys.p;
+  c->key_slots = nkeys;
+  const uint8_t* din = (const uint8_t*)c->h_in.p;
+  const uint8_t* dad = (const uint8_t*)c->h_aad.p;
+  uint8_t* dout = (uint8_t*)c->h_out.p;
+  uint32_t* dst = (uint32_t*)c->h_status.p;
+  switch (mode) {
+    case WG_MODE_SEAL:
+      rc = launch_tiles<WG_MODE_SEAL, true>(c, c->h_desc.p, n, din, in_size, dad, aad_size, dout, out_size, nullptr, max_len, 0, s);
+      break;
+    case WG_MODE_OPEN:
+      rc = launch_tiles<WG_MODE_OPEN, true>(c, c->h_desc.p, n, din, in_size, dad, aad_size, dout, out_size, dst, max_len, 0, s);
+      break;
+    case WG_MODE_CIPHER:
+      rc = launch_tiles<WG_MODE_CIPHER, true>(c, c->h_desc.p, n, din, in_size, nullptr, 0, dout, out_size, nullptr, max_len, 0, s);
+      break;
+    case WG_MODE_MAC:
+      rc = launch_tiles<WG_MODE_MAC, true>(c, c->h_desc.p, n, din, in_size, nullptr, 0, dout, out_size, nullptr, max_len, 0, s);
+      break;
+    default:
+      rc = fail(WG_EINVAL, "unknown mode %d", mode);
+  }
+  c->keys = saved_keys;
+  c->key_slots = saved_slots;
+  if (rc) return rc;
+  if (mode == WG_MODE_OPEN) HIPTRY(hipMemcpyAsync(status, dst, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, s));
+  HIPTRY(hipMemcpyAsync(out, dout, out_size, hipMemcpyDeviceToHost, s));
+  HIPTRY(hipMemsetAsync(c->h_keys.p, 0, (size_t)nkeys * 32, s));  // do not leave key material behind
+  HIPTRY(hipStreamSynchronize(s));
+  return WG_OK;
+}
+
+// ---- instrumentation -----------------------------------------------------------
+
+int wg_timing_enable(wg_ctx* c, int on) {
+  if (!c) return fail(WG_EINVAL, "NULL context");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->timing = on != 0;
+  return WG_OK;
+}
+
+int wg_timing_read(wg_ctx* c, double* total_ms, uint64_t* launches) {
+  if (!c) return fail(WG_EINVAL, "NULL context");
+  DeviceGuard g(c->device);
+  std::lock_guard<std::mutex> lk(c->mu);
+  for (auto& e : c->events) {
+    float ms = 0;
+    HIPTRY(hipEventSynchronize(e.second));
+    HIPTRY(hipEventElapsedTime(&ms, e.first, e.second));
+    c->timed_ms += ms;
+    c->timed_launches += 1;
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  c->events.clear();
+  if (total_ms) *total_ms = c->timed_ms;
+  if (launches) *launches = c->timed_launches;
+  c->timed_ms = 0;
+  c->timed_launches = 0;
+  return WG_OK;
+}
+
+// ---- self test: the reference's own known-answer vectors, run on the device ----
+
+int wg_aead_selftest(int device) {
+  wg_ctx* c = nullptr;
+  if (wg_ctx_create(device, 1, &c) != WG_OK) return 0;
+  int ok = 1;
+  // RFC 8439 2.8.2 (Poly1305Test.java:151-199)
+  static const uint8_t key[32] = {0x80, 0x81, 0x82, 0x83, 0x84, 0x85, 0x86, 0x87, 0x88, 0x89, 0x8a,
+                                  0x8b, 0x8c, 0x8d, 0x8e, 0x8f, 0x90, 0x91, 0x92, 0x93, 0x94, 0x95,
+                                  0x96, 0x97, 0x98, 0x99, 0x9a, 0x9b, 0x9c, 0x9d, 0x9e, 0x9f};
+  static const uint8_t aad[12] = {0x50, 0x51, 0x52, 0x53, 0xc0, 0xc1, 0xc2, 0xc3, 0xc4, 0xc5, 0xc6, 0xc7};
+  static const char* pt = "Ladies and Gentlemen of the class of '99: If I could offer you only one tip for the future, sunscreen would be it.";
+  static const uint8_t tag_expect[16] = {0x1a, 0xe1, 0x0b, 0x59, 0x4f, 0x09, 0xe2, 0x6a,
+                                         0x7e, 0x90, 0x2e, 0xcb, 0xd0, 0x60, 0x06, 0x91};
+  static const uint8_t ct_head[8] = {0xd3, 0x1a, 0x8d, 0x34, 0x64, 0x8e, 0x60, 0xdb};
+  const uint32_t L = (uint32_t)strlen(pt);
+  wg_aead_desc d{};
+  d.len = L;
+  d.aad_len = 12;
+  d.nonce[0] = 0x00000007u;  // 07 00 00 00 | 40 41 42 43 | 44 45 46 47
+  d.nonce[1] = 0x43424140u;
+  d.nonce[2] = 0x47464544u;
+  std::vector<uint8_t> out(L + 16, 0);
+  if (wg_aead_host(c, WG_MODE_SEAL, &d, 1, key, 1, (const uint8_t*)pt, L, aad, 12, out.data(), out.size(), nullptr) != WG_OK ||
+      memcmp(out.data() + L, tag_expect, 16) != 0 || memcmp(out.data(), ct_head, 8) != 0)
+    ok = 0;
+  // RFC 8439 2.5.2 Poly1305 (Poly1305Test.java:49-61)
+  static const uint8_t pkey[32] = {0x85, 0xd6, 0xbe, 0x78, 0x57, 0x55, 0x6d, 0x33, 0x7f, 0x44, 0x52,
+                                   0xfe, 0x42, 0xd5, 0x06, 0xa8, 0x01, 0x03, 0x80, 0x8a, 0xfb, 0x0d,
+                                   0xb2, 0xfd, 0x4a, 0xbf, 0xf6, 0xaf, 0x41, 0x49, 0xf5, 0x1b};
+  static const char* msg = "Cryptographic Forum Research Group";
+  static const uint8_t mac_expect[16] = {0xa8, 0x06, 0x1d, 0xc1, 0x30, 0x51, 0x36, 0xc6,
+                                         0xc2, 0x2b, 0x8b, 0xaf, 0x0c, 0x01, 0x27, 0xa9};
+  wg_aead_desc m{};
+  m.len = (uint32_t)strlen(msg);
+  uint8_t mac[16] = {0};
+  if (wg_aead_host(c, WG_MODE_MAC, &m, 1, pkey, 1, (const uint8_t*)msg, m.len, nullptr, 0, mac, 16, nullptr) != WG_OK ||
+      memcmp(mac, mac_expect, 16) != 0)
+    ok = 0;
+  // donna wrap vector: a final value of 2^130 - 2 (poly1305-donna.c:118-134)
+  uint8_t wkey[32] = {2};
+  uint8_t wmsg[16];
+  memset(wmsg, 0xff, 16);
+  static const uint8_t wmac[16] = {3};
+  wg_aead_desc w{};
+  w.len = 16;
+  if (wg_aead_host(c, WG_MODE_MAC, &w, 1, wkey, 1, wmsg, 16, nullptr, 0, mac, 16, nullptr) != WG_OK ||
+      memcmp(mac, wmac, 16) != 0)
+    ok = 0;
+  wg_ctx_destroy(c);
+  return ok;
+}
+
+}  // extern "C"

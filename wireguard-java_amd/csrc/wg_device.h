@@ -1,0 +1,143 @@
+// wg_device.h — gfx950 device arithmetic for the transport AEAD.
+//
+// ChaCha20 block (RFC 8439 2.3) restated for 64-wide CDNA4 waves: one lane owns
+// one 64-byte counter block in 16 VGPRs. Reference semantics:
+//   chacha_permute / chacha_block_generic  ax.xz.wireguard.noise/src/main/c/chacha-generic.c:10-78
+//   state layout (constants, key, ctr, nonce) ChaCha20.java:247-266
+// Poly1305 (RFC 8439 2.5) in radix 2^26 (5 limbs in VGPRs) with v_mad_u64_u32
+// products; canonical final reduction as poly1305-donna-64.h:154-223.
+//
+// Measured on MI355X (tools/microbench2.hip): v_add/v_xor issue at
+// ~60 T lane-op/s, every shift/rotate/perm/3-operand op at ~35 T, v_mad_u64_u32 at
+// ~30 T. The rotates therefore set the ChaCha20 cost; 16/8-bit rotates use
+// v_perm_b32 (measured 1-3% ahead of v_alignbit_b32).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace wgd {
+
+constexpr uint32_t M26 = 0x3ffffffu;
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
+__device__ __forceinline__ uint32_t rotl16(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x01000302u); }
+__device__ __forceinline__ uint32_t rotl8(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x02010003u); }
+
+#define WG_QR(a, b, c, d)                \
+  a += b; d ^= a; d = rotl16(d);         \
+  c += d; b ^= c; b = rotl(b, 12);       \
+  a += b; d ^= a; d = rotl8(d);          \
+  c += d; b ^= c; b = rotl(b, 7);
+
+// Keystream block for (key, 32-bit block counter, nonce words n0..n2).
+// out[i] = permute(state)[i] + state[i], i.e. little-endian keystream words.
+__device__ __forceinline__ void chacha20_block(const uint32_t k[8], uint32_t ctr, uint32_t n0, uint32_t n1,
+                                               uint32_t n2, uint32_t out[16]) {
+  uint32_t x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
+  uint32_t x4 = k[0], x5 = k[1], x6 = k[2], x7 = k[3], x8 = k[4], x9 = k[5], x10 = k[6], x11 = k[7];
+  uint32_t x12 = ctr, x13 = n0, x14 = n1, x15 = n2;
+#pragma unroll 2
+  for (int r = 0; r < 10; ++r) {
+    WG_QR(x0, x4, x8, x12) WG_QR(x1, x5, x9, x13) WG_QR(x2, x6, x10, x14) WG_QR(x3, x7, x11, x15)
+    WG_QR(x0, x5, x10, x15) WG_QR(x1, x6, x11, x12) WG_QR(x2, x7, x8, x13) WG_QR(x3, x4, x9, x14)
+  }
+  out[0] = x0 + 0x61707865u; out[1] = x1 + 0x3320646eu; out[2] = x2 + 0x79622d32u; out[3] = x3 + 0x6b206574u;
+  out[4] = x4 + k[0]; out[5] = x5 + k[1]; out[6] = x6 + k[2]; out[7] = x7 + k[3];
+  out[8] = x8 + k[4]; out[9] = x9 + k[5]; out[10] = x10 + k[6]; out[11] = x11 + k[7];
+  out[12] = x12 + ctr; out[13] = x13 + n0; out[14] = x14 + n1; out[15] = x15 + n2;
+}
+#undef WG_QR
+
+// ---- Poly1305, radix 2^26 -------------------------------------------------
+// An element of Z/(2^130-5) as 5 limbs h[i] (value = sum h[i] 2^(26 i)), kept
+// partially reduced (limbs < 2^26 + 2^8 after poly_mul; < 2^27 after adding one
+// message block).
+
+// 16 message bytes (four LE words) -> limbs; hibit = 1<<24 adds 2^128 (full block).
+__device__ __forceinline__ void poly_block_limbs(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t hibit,
+                                                 uint32_t c[5]) {
+  c[0] = w0 & M26;
+  c[1] = __builtin_amdgcn_alignbit(w1, w0, 26) & M26;
+  c[2] = __builtin_amdgcn_alignbit(w2, w1, 20) & M26;
+  c[3] = __builtin_amdgcn_alignbit(w3, w2, 14) & M26;
+  c[4] = (w3 >> 8) | hibit;
+}
+
+// r from the first 16 bytes of the one-time key, clamped as in
+// poly1305-donna-64.h:80-86 (r &= 0x0ffffffc0ffffffc0ffffffc0fffffff).
+__device__ __forceinline__ void poly_r_limbs(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3, uint32_t r[5]) {
+  poly_block_limbs(k0 & 0x0fffffffu, k1 & 0x0ffffffcu, k2 & 0x0ffffffcu, k3 & 0x0ffffffcu, 0u, r);
+}
+
+// h = h * r mod 2^130-5 (partial reduction). s[i] = 5 * r[i] for i = 1..4.
+// Bounds: h limbs < 2^27, r limbs < 2^26 => each d_i < 2^58 (so the 26-bit
+// carries fit 32 bits) and the wrap carry from d4 is < 2^29.3 (so 5c < 2^32).
+__device__ __forceinline__ void poly_mul(uint32_t h[5], const uint32_t r[5], const uint32_t s[5]) {
+  uint64_t d0 = (uint64_t)h[0] * r[0] + (uint64_t)h[1] * s[4] + (uint64_t)h[2] * s[3] + (uint64_t)h[3] * s[2] +
+                (uint64_t)h[4] * s[1];
+  uint64_t d1 = (uint64_t)h[0] * r[1] + (uint64_t)h[1] * r[0] + (uint64_t)h[2] * s[4] + (uint64_t)h[3] * s[3] +
+                (uint64_t)h[4] * s[2];
+  uint64_t d2 = (uint64_t)h[0] * r[2] + (uint64_t)h[1] * r[1] + (uint64_t)h[2] * r[0] + (uint64_t)h[3] * s[4] +
+                (uint64_t)h[4] * s[3];
+  uint64_t d3 = (uint64_t)h[0] * r[3] + (uint64_t)h[1] * r[2] + (uint64_t)h[2] * r[1] + (uint64_t)h[3] * r[0] +
+                (uint64_t)h[4] * s[4];
+  uint64_t d4 = (uint64_t)h[0] * r[4] + (uint64_t)h[1] * r[3] + (uint64_t)h[2] * r[2] + (uint64_t)h[3] * r[1] +
+                (uint64_t)h[4] * r[0];
+  uint32_t c;
+  c = (uint32_t)(d0 >> 26); h[0] = (uint32_t)d0 & M26; d1 += c;
+  c = (uint32_t)(d1 >> 26); h[1] = (uint32_t)d1 & M26; d2 += c;
+  c = (uint32_t)(d2 >> 26); h[2] = (uint32_t)d2 & M26; d3 += c;
+  c = (uint32_t)(d3 >> 26); h[3] = (uint32_t)d3 & M26; d4 += c;
+  c = (uint32_t)(d4 >> 26); h[4] = (uint32_t)d4 & M26;
+  h[0] += c * 5u;
+  c = h[0] >> 26; h[0] &= M26;
+  h[1] += c;
+}
+
+__device__ __forceinline__ void poly_scale5(const uint32_t r[5], uint32_t s[5]) {
+  s[0] = 0;
+  s[1] = r[1] * 5u; s[2] = r[2] * 5u; s[3] = r[3] * 5u; s[4] = r[4] * 5u;
+}
+
+// Full carry, canonical reduction (h < p), + s mod 2^128 -> tag words.
+// Input limbs may be as large as 2^32 - 1 (sum of up to 63 partial products).
+__device__ __forceinline__ void poly_finish(uint32_t h[5], uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
+                                            uint32_t tag[4]) {
+  uint32_t c;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    c = h[0] >> 26; h[0] &= M26; h[1] += c;
+    c = h[1] >> 26; h[1] &= M26; h[2] += c;
+    c = h[2] >> 26; h[2] &= M26; h[3] += c;
+    c = h[3] >> 26; h[3] &= M26; h[4] += c;
+    c = h[4] >> 26; h[4] &= M26; h[0] += c * 5u;
+  }
+  // non-wrapping normalisation: limbs 0..3 canonical, h4 <= 2^26, so h < 2p
+  c = h[0] >> 26; h[0] &= M26; h[1] += c;
+  c = h[1] >> 26; h[1] &= M26; h[2] += c;
+  c = h[2] >> 26; h[2] &= M26; h[3] += c;
+  c = h[3] >> 26; h[3] &= M26; h[4] += c;
+  // g = h + 5 - 2^130; take g when it does not borrow (h >= p)
+  uint32_t g0 = h[0] + 5u; c = g0 >> 26; g0 &= M26;
+  uint32_t g1 = h[1] + c; c = g1 >> 26; g1 &= M26;
+  uint32_t g2 = h[2] + c; c = g2 >> 26; g2 &= M26;
+  uint32_t g3 = h[3] + c; c = g3 >> 26; g3 &= M26;
+  uint32_t g4 = h[4] + c - (1u << 26);
+  uint32_t mask = (g4 >> 31) - 1u;  // all ones if h >= p
+  h[0] = (h[0] & ~mask) | (g0 & mask);
+  h[1] = (h[1] & ~mask) | (g1 & mask);
+  h[2] = (h[2] & ~mask) | (g2 & mask);
+  h[3] = (h[3] & ~mask) | (g3 & mask);
+  h[4] = (h[4] & ~mask) | (g4 & mask);
+  // h mod 2^128 as four words, then + s
+  uint32_t w0 = h[0] | (h[1] << 26);
+  uint32_t w1 = (h[1] >> 6) | (h[2] << 20);
+  uint32_t w2 = (h[2] >> 12) | (h[3] << 14);
+  uint32_t w3 = (h[3] >> 18) | (h[4] << 8);
+  uint64_t f = (uint64_t)w0 + s0; tag[0] = (uint32_t)f;
+  f = (uint64_t)w1 + s1 + (f >> 32); tag[1] = (uint32_t)f;
+  f = (uint64_t)w2 + s2 + (f >> 32); tag[2] = (uint32_t)f;
+  f = (uint64_t)w3 + s3 + (f >> 32); tag[3] = (uint32_t)f;
+}
+
+}  // namespace wgd

@@ -1,0 +1,180 @@
+"""Device context and the batched transport API over libwgaead.
+
+``Engine`` owns one ``wg_ctx`` (one HIP device, its stream and device key
+table). It is the MI355X-side counterpart of the reference's per-packet
+ForkJoinPool dispatch (TransportManager.java:41,70-93,137-158): packets are
+sealed/opened in batches that stay resident in HBM.
+
+Descriptors are ``wg_pkt`` records (include/wgaead.h). On the torch side a
+batch of them is an int64 tensor of shape [n, 4]: (in_off, out_off, counter,
+len | key_slot << 32) — byte-identical to the C struct array.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+
+import numpy as np
+
+from . import _lib as L
+
+WG_PKT_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("counter", "<u8"), ("len", "<u4"),
+                         ("key_slot", "<u4")])
+
+
+def pack_desc(in_off, out_off, counter, length, key_slot) -> np.ndarray:
+    """Build a wg_pkt array (numpy structured) from per-packet columns."""
+    n = len(np.atleast_1d(in_off))
+    d = np.zeros(n, WG_PKT_DTYPE)
+    d["in_off"], d["out_off"], d["counter"] = in_off, out_off, counter
+    d["len"], d["key_slot"] = length, key_slot
+    return d
+
+
+def desc_as_int64(d: np.ndarray) -> np.ndarray:
+    """wg_pkt array viewed as int64 [n, 4] (for torch.from_numpy)."""
+    return np.ascontiguousarray(d).view(np.int64).reshape(-1, 4)
+
+
+class Engine:
+    """One HIP device: stream, key table (``key_slots`` x 32 bytes) and batch entry points."""
+
+    def __init__(self, device: int = 0, key_slots: int = 1024):
+        self._lib = L.lib()
+        ctx = ctypes.c_void_p()
+        L.check(self._lib.wg_ctx_create(device, key_slots, ctypes.byref(ctx)))
+        self.ctx = ctx
+        self.device = device
+        self.key_slots = key_slots
+        self._free = list(range(key_slots - 1, -1, -1))
+        self._slot_lock = threading.Lock()
+
+    # ---- lifecycle --------------------------------------------------------------
+    def close(self):
+        if self.ctx:
+            self._lib.wg_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> int:
+        return self._lib.wg_ctx_stream(self.ctx)
+
+    def sync(self, stream: int | None = None):
+        L.check(self._lib.wg_sync(self.ctx, stream))
+
+    # ---- keys (SymmetricKeypair.java:39-50, 85-93) ------------------------------
+    def alloc_slots(self, n: int) -> list[int]:
+        with self._slot_lock:
+            if len(self._free) < n:
+                raise L.WgError(L.WG_ERANGE, "key table full")
+            return [self._free.pop() for _ in range(n)]
+
+    def free_slots(self, slots):
+        for s in slots:
+            self.zero_keys(s, 1)
+        with self._slot_lock:
+            self._free.extend(slots)
+
+    def set_keys(self, first_slot: int, keys) -> None:
+        k = np.ascontiguousarray(np.frombuffer(bytes(keys), np.uint8) if not isinstance(keys, np.ndarray) else keys,
+                                 dtype=np.uint8)
+        assert k.size % 32 == 0
+        L.check(self._lib.wg_keys_set(self.ctx, first_slot, k.size // 32, k.ctypes.data))
+
+    def zero_keys(self, first_slot: int, n: int) -> None:
+        L.check(self._lib.wg_keys_zero(self.ctx, first_slot, n))
+
+    # ---- device-resident batches (torch tensors on this device) -------------------
+    def seal(self, desc, inp, out, max_len: int, uniform: bool = False, stream: int | None = None):
+        """wg_seal_batch over torch tensors: desc int64 [n,4], inp/out uint8 (device)."""
+        n = desc.shape[0]
+        L.check(self._lib.wg_seal_batch(self.ctx, desc.data_ptr(), n, inp.data_ptr(), inp.numel(), out.data_ptr(),
+                                        out.numel(), max_len, L.WG_F_UNIFORM if uniform else 0,
+                                        stream if stream is not None else _torch_stream()))
+
+    def open(self, desc, inp, out, status, max_len: int, uniform: bool = False, stream: int | None = None):
+        """wg_open_batch; `status` is an int32/uint32 device tensor of n entries (0 ok, 1 bad tag)."""
+        n = desc.shape[0]
+        L.check(self._lib.wg_open_batch(self.ctx, desc.data_ptr(), n, inp.data_ptr(), inp.numel(), out.data_ptr(),
+                                        out.numel(), status.data_ptr(), max_len, L.WG_F_UNIFORM if uniform else 0,
+                                        stream if stream is not None else _torch_stream()))
+
+    # ---- host buffers ---------------------------------------------------------------
+    def seal_host(self, desc: np.ndarray, inp: np.ndarray, out: np.ndarray, max_len: int, uniform: bool = False):
+        d = np.ascontiguousarray(desc)
+        L.check(self._lib.wg_seal_host(self.ctx, d.ctypes.data, len(d), inp.ctypes.data, inp.nbytes, out.ctypes.data,
+                                       out.nbytes, max_len, L.WG_F_UNIFORM if uniform else 0))
+
+    def open_host(self, desc: np.ndarray, inp: np.ndarray, out: np.ndarray, max_len: int,
+                  uniform: bool = False) -> np.ndarray:
+        d = np.ascontiguousarray(desc)
+        status = np.zeros(len(d), np.uint32)
+        L.check(self._lib.wg_open_host(self.ctx, d.ctypes.data, len(d), inp.ctypes.data, inp.nbytes, out.ctypes.data,
+                                       out.nbytes, status.ctypes.data, max_len, L.WG_F_UNIFORM if uniform else 0))
+        return status
+
+    def aead_host(self, mode: int, descs, keys: bytes, inp: bytes, aad: bytes, out_size: int):
+        """General AEAD / primitive batch on host buffers (wg_aead_host). Returns (out, status)."""
+        arr = (L.WgAeadDesc * len(descs))(*descs)
+        kb = np.frombuffer(keys, np.uint8).copy()
+        ib = np.frombuffer(inp, np.uint8).copy() if inp else np.zeros(1, np.uint8)
+        ab = np.frombuffer(aad, np.uint8).copy() if aad else np.zeros(1, np.uint8)
+        out = np.zeros(max(out_size, 1), np.uint8)
+        status = np.zeros(len(descs), np.uint32)
+        L.check(self._lib.wg_aead_host(self.ctx, mode, ctypes.addressof(arr), len(descs), kb.ctypes.data,
+                                       kb.size // 32, ib.ctypes.data, len(inp), ab.ctypes.data, len(aad),
+                                       out.ctypes.data, out_size, status.ctypes.data))
+        return out[:out_size].tobytes(), status
+
+    def seal1(self, slot: int, counter: int, pt: bytes) -> bytes:
+        src = np.frombuffer(pt, np.uint8).copy() if pt else np.zeros(1, np.uint8)
+        out = np.zeros(len(pt) + 16, np.uint8)
+        L.check(self._lib.wg_seal1(self.ctx, slot, counter, src.ctypes.data, len(pt), out.ctypes.data))
+        return out.tobytes()
+
+    def open1(self, slot: int, counter: int, ct_tag: bytes) -> bytes | None:
+        n = len(ct_tag) - 16
+        src = np.frombuffer(ct_tag, np.uint8).copy()
+        out = np.zeros(max(n, 1), np.uint8)
+        rc = L.check(self._lib.wg_open1(self.ctx, slot, counter, src.ctypes.data, n, out.ctypes.data))
+        return None if rc == 1 else out[:n].tobytes()
+
+    # ---- instrumentation ----------------------------------------------------------
+    def timing(self, on: bool):
+        L.check(self._lib.wg_timing_enable(self.ctx, 1 if on else 0))
+
+    def timing_read(self) -> tuple[float, int]:
+        ms = ctypes.c_double()
+        k = ctypes.c_uint64()
+        L.check(self._lib.wg_timing_read(self.ctx, ctypes.byref(ms), ctypes.byref(k)))
+        return ms.value, k.value
+
+
+def _torch_stream() -> int:
+    import torch
+    return torch.cuda.current_stream().cuda_stream
+
+
+def selftest(device: int = 0) -> bool:
+    """wg_aead_selftest: the reference's known-answer vectors, on the device (Poly1305.java:62-76)."""
+    return L.lib().wg_aead_selftest(device) == 1
+
+
+_default: dict[int, Engine] = {}
+_default_lock = threading.Lock()
+
+
+def default_engine(device: int | None = None) -> Engine:
+    """Process-wide engine per device, created on first use (like the reference's static initialisers)."""
+    import os
+    dev = int(os.environ.get("WG_DEVICE", "0")) if device is None else device
+    with _default_lock:
+        if dev not in _default:
+            _default[dev] = Engine(dev, key_slots=int(os.environ.get("WG_KEY_SLOTS", "65536")))
+        return _default[dev]
