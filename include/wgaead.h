@@ -16,7 +16,8 @@
  *    status array (WG_PKT_BADTAG), mirroring the per-packet
  *    AEADBadTagException of NOISE/crypto/ChaCha20Poly1305.java:51-53.
  *  - "batch" calls take DEVICE pointers and are asynchronous on `stream`
- *    (a hipStream_t passed as void*; NULL = the context's own stream).
+ *    (a hipStream_t passed as void*, used as-is: NULL is HIP's default stream;
+ *    wg_ctx_stream(ctx) returns the context's own non-blocking stream).
  *    The "host" calls take host pointers and return after completion.
  *  - Packets are independent (no cross-packet state): a batch shards freely
  *    across devices; no collective is involved (one wg_ctx per device).

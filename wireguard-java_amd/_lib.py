@@ -11,7 +11,7 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libwgaead.so")
+LIB_PATH = os.environ.get("WG_LIB_PATH") or os.path.join(HERE, "libwgaead.so")
 
 WG_OK = 0
 WG_EINVAL = -22

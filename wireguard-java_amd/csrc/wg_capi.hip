@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -21,6 +22,9 @@
 namespace {
 
 thread_local std::string g_err;
+#ifdef WG_DIAG
+uint64_t* g_stamps = nullptr;
+#endif
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -101,12 +105,36 @@ uint32_t host_pkt_blocks(uint32_t len) {
 
 constexpr uint32_t kLdsBudget = 64u * 1024u;  // per workgroup; keeps >= 2 tiles per CU
 
-// lanes per packet for the Poly1305 phase: fill one wave with the tile's packets
+// Tunables (environment, read once): WG_TILE_PASSES = max workgroup passes per
+// uniform tile (1..4, default 2); WG_POLY_WAVES = waves the Poly1305 phase spreads
+// a tile's packets over (1..4, default 4); WG_POLY_GMAX = cap on lanes per packet.
+struct Tunables {
+  uint32_t tile_passes = 2, poly_waves = 4, poly_gmax = 16;
+  uint32_t stream_ppw_uniform = 8, stream_ppw_mixed = 16;  // packets per wave in k_stream
+  int use_tile_for_transport = 0;                           // 1: route transport batches to k_tile
+  Tunables() {
+    if (const char* e = getenv("WG_STREAM_PPW")) stream_ppw_uniform = stream_ppw_mixed = std::max(1, atoi(e));
+    if (const char* e = getenv("WG_STREAM_PPW_MIXED")) stream_ppw_mixed = std::max(1, atoi(e));
+    if (const char* e = getenv("WG_TRANSPORT_KERNEL")) use_tile_for_transport = strcmp(e, "tile") == 0;
+    if (const char* e = getenv("WG_TILE_PASSES")) tile_passes = std::min(4u, std::max(1u, (uint32_t)atoi(e)));
+    if (const char* e = getenv("WG_POLY_WAVES")) poly_waves = std::min(4u, std::max(1u, (uint32_t)atoi(e)));
+    if (const char* e = getenv("WG_POLY_GMAX")) poly_gmax = std::min(64u, std::max(1u, (uint32_t)atoi(e)));
+  }
+};
+const Tunables& tunables() {
+  static Tunables t;
+  return t;
+}
+
+// lanes per packet for the Poly1305 phase: spread the tile's packets over
+// `poly_waves` waves (groups never straddle a wave)
 uint32_t choose_poly_g(uint32_t ppt) {
   if (ppt == 0) return 1;
-  uint32_t g = 64u / ppt;
+  const Tunables& t = tunables();
+  uint32_t per_wave = (ppt + t.poly_waves - 1) / t.poly_waves;
+  uint32_t g = 64u / per_wave;
   if (g < 1) g = 1;
-  if (g > 16) g = 16;
+  if (g > t.poly_gmax) g = t.poly_gmax;
   return g;
 }
 
@@ -158,7 +186,7 @@ int launch_tiles(wg_ctx* c, const void* desc, uint32_t n, const uint8_t* in, uin
     } else if (nb <= WG_TPB) {
       // pick the tile size (1 or 2 passes of the workgroup) that idles fewest lanes
       double best = -1;
-      for (uint32_t k = 1; k <= 2; ++k) {
+      for (uint32_t k = 1; k <= tunables().tile_passes; ++k) {
         uint32_t p = k * WG_TPB / nb;
         uint32_t img = p * (nb - aead_extra) * 64u;
         if (p == 0 || wgk::tile_header_bytes(p) + img > kLdsBudget) continue;
@@ -210,6 +238,9 @@ int launch_tiles(wg_ctx* c, const void* desc, uint32_t n, const uint8_t* in, uin
     grid = max_tiles;
   }
   if (lds > 160u * 1024u) return fail(WG_E2BIG, "tile needs %u bytes of LDS", lds);
+#ifdef WG_DIAG
+  P.stamps = g_stamps;
+#endif
   hipEvent_t ev;
   record_start(c, s, &ev);
   hipLaunchKernelGGL((wgk::k_tile<MODE, GENERAL>), dim3(grid), dim3(WG_TPB), lds, s, P);
@@ -219,11 +250,59 @@ int launch_tiles(wg_ctx* c, const void* desc, uint32_t n, const uint8_t* in, uin
   return WG_OK;
 }
 
-hipStream_t pick_stream(wg_ctx* c, void* stream) { return stream ? (hipStream_t)stream : c->stream; }
+// the caller's stream as-is: NULL is HIP's default (null) stream, like every HIP API;
+// pass wg_ctx_stream(ctx) to use the context's own non-blocking stream
+// Transport seal/open through k_stream (one wave per workgroup, 8 packet slots).
+template <int MODE>
+int launch_stream(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, uint64_t in_size, uint8_t* out,
+                  uint64_t out_size, uint32_t* status, uint32_t max_len, uint32_t flags, hipStream_t s) {
+  if (n == 0) return WG_OK;
+  if (!desc || (((uintptr_t)desc) & 15u)) return fail(WG_EINVAL, "descriptor array must be non-NULL and 16-byte aligned");
+  if (!in || !out) return fail(WG_EINVAL, "NULL buffer");
+  if (max_len > WG_MAX_PACKET) return fail(WG_E2BIG, "max_len %u > WG_MAX_PACKET", max_len);
+  wgk::StreamParams P{};
+  P.desc = desc;
+  P.n = n;
+  P.ppw = (flags & WG_F_UNIFORM) ? tunables().stream_ppw_uniform : tunables().stream_ppw_mixed;
+  P.max_len = max_len;
+  P.key_slots = c->key_slots;
+  P.in = in;
+  P.in_size = in_size;
+  P.out = out;
+  P.out_size = out_size;
+  P.keys = c->keys;
+  P.status = status;
+  const uint32_t grid = (n + P.ppw - 1) / P.ppw;
+  hipEvent_t ev;
+  record_start(c, s, &ev);
+  hipLaunchKernelGGL((wgk::k_stream<MODE>), dim3(grid), dim3(64), 0, s, P);
+  hipError_t e = hipGetLastError();
+  record_end(c, s, ev);
+  if (e != hipSuccess) return fail(WG_EDEVICE, "k_stream launch: %s", hipGetErrorString(e));
+  return WG_OK;
+}
+
+template <int MODE>
+int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, uint64_t in_size, uint8_t* out,
+                     uint64_t out_size, uint32_t* status, uint32_t max_len, uint32_t flags, hipStream_t s) {
+  if (tunables().use_tile_for_transport)
+    return launch_tiles<MODE, false>(c, desc, n, in, in_size, nullptr, 0, out, out_size, status, max_len, flags, s);
+  return launch_stream<MODE>(c, desc, n, in, in_size, out, out_size, status, max_len, flags, s);
+}
+
+hipStream_t pick_stream(wg_ctx*, void* stream) { return (hipStream_t)stream; }
 
 }  // namespace
 
 extern "C" {
+
+#ifdef WG_DIAG
+// diagnostic build only: device buffer of 8 x u64 per workgroup for phase stamps
+int wg_diag_stamps(void* dev_buf) {
+  g_stamps = (uint64_t*)dev_buf;
+  return WG_OK;
+}
+#endif
 
 const char* wg_last_error(void) { return g_err.c_str(); }
 const char* wg_version(void) { return "wgaead 0.1.0 gfx950"; }
@@ -307,8 +386,8 @@ int wg_seal_batch(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
   if (!c) return fail(WG_EINVAL, "NULL context");
   DeviceGuard g(c->device);
   std::lock_guard<std::mutex> lk(c->mu);
-  return launch_tiles<WG_MODE_SEAL, false>(c, desc, n, in, in_size, nullptr, 0, out, out_size, nullptr, max_len, flags,
-                                           pick_stream(c, stream));
+  return launch_transport<WG_MODE_SEAL>(c, desc, n, in, in_size, out, out_size, nullptr, max_len, flags,
+                                       pick_stream(c, stream));
 }
 
 int wg_open_batch(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, uint64_t in_size, uint8_t* out,
@@ -316,8 +395,8 @@ int wg_open_batch(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
   if (!c) return fail(WG_EINVAL, "NULL context");
   DeviceGuard g(c->device);
   std::lock_guard<std::mutex> lk(c->mu);
-  return launch_tiles<WG_MODE_OPEN, false>(c, desc, n, in, in_size, nullptr, 0, out, out_size, status, max_len, flags,
-                                           pick_stream(c, stream));
+  return launch_transport<WG_MODE_OPEN>(c, desc, n, in, in_size, out, out_size, status, max_len, flags,
+                                       pick_stream(c, stream));
 }
 
 int wg_aead_batch(wg_ctx* c, int mode, const wg_aead_desc* desc, uint32_t n, const uint8_t* in, uint64_t in_size,
@@ -360,12 +439,12 @@ static int host_transport(wg_ctx* c, bool open, const wg_pkt* desc, uint32_t n, 
   if (open) {
     // the caller's plaintext buffer must stay untouched on failure: stage it
     HIPTRY(hipMemcpyAsync(c->h_out.p, out, out_size, hipMemcpyHostToDevice, s));
-    rc = launch_tiles<WG_MODE_OPEN, false>(c, c->h_desc.p, n, (const uint8_t*)c->h_in.p, in_size, nullptr, 0,
-                                           (uint8_t*)c->h_out.p, out_size, (uint32_t*)c->h_status.p, max_len, flags, s);
+    rc = launch_transport<WG_MODE_OPEN>(c, (const wg_pkt*)c->h_desc.p, n, (const uint8_t*)c->h_in.p, in_size,
+                                        (uint8_t*)c->h_out.p, out_size, (uint32_t*)c->h_status.p, max_len, flags, s);
   } else {
     HIPTRY(hipMemcpyAsync(c->h_out.p, out, out_size, hipMemcpyHostToDevice, s));
-    rc = launch_tiles<WG_MODE_SEAL, false>(c, c->h_desc.p, n, (const uint8_t*)c->h_in.p, in_size, nullptr, 0,
-                                           (uint8_t*)c->h_out.p, out_size, nullptr, max_len, flags, s);
+    rc = launch_transport<WG_MODE_SEAL>(c, (const wg_pkt*)c->h_desc.p, n, (const uint8_t*)c->h_in.p, in_size,
+                                        (uint8_t*)c->h_out.p, out_size, nullptr, max_len, flags, s);
   }
   if (rc) return rc;
   if (open) HIPTRY(hipMemcpyAsync(status, c->h_status.p, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, s));

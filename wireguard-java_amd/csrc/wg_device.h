@@ -72,23 +72,26 @@ __device__ __forceinline__ void poly_r_limbs(uint32_t k0, uint32_t k1, uint32_t 
 // h = h * r mod 2^130-5 (partial reduction). s[i] = 5 * r[i] for i = 1..4.
 // Bounds: h limbs < 2^27, r limbs < 2^26 => each d_i < 2^58 (so the 26-bit
 // carries fit 32 bits) and the wrap carry from d4 is < 2^29.3 (so 5c < 2^32).
+// Each limb's carry seeds the next limb's v_mad_u64_u32 accumulator chain, so a
+// step costs 25 mads + 5 alignbits + 5 ands (+ the 2^130 wrap) and no 64-bit adds.
 __device__ __forceinline__ void poly_mul(uint32_t h[5], const uint32_t r[5], const uint32_t s[5]) {
-  uint64_t d0 = (uint64_t)h[0] * r[0] + (uint64_t)h[1] * s[4] + (uint64_t)h[2] * s[3] + (uint64_t)h[3] * s[2] +
-                (uint64_t)h[4] * s[1];
-  uint64_t d1 = (uint64_t)h[0] * r[1] + (uint64_t)h[1] * r[0] + (uint64_t)h[2] * s[4] + (uint64_t)h[3] * s[3] +
-                (uint64_t)h[4] * s[2];
-  uint64_t d2 = (uint64_t)h[0] * r[2] + (uint64_t)h[1] * r[1] + (uint64_t)h[2] * r[0] + (uint64_t)h[3] * s[4] +
-                (uint64_t)h[4] * s[3];
-  uint64_t d3 = (uint64_t)h[0] * r[3] + (uint64_t)h[1] * r[2] + (uint64_t)h[2] * r[1] + (uint64_t)h[3] * r[0] +
-                (uint64_t)h[4] * s[4];
-  uint64_t d4 = (uint64_t)h[0] * r[4] + (uint64_t)h[1] * r[3] + (uint64_t)h[2] * r[2] + (uint64_t)h[3] * r[1] +
-                (uint64_t)h[4] * r[0];
-  uint32_t c;
-  c = (uint32_t)(d0 >> 26); h[0] = (uint32_t)d0 & M26; d1 += c;
-  c = (uint32_t)(d1 >> 26); h[1] = (uint32_t)d1 & M26; d2 += c;
-  c = (uint32_t)(d2 >> 26); h[2] = (uint32_t)d2 & M26; d3 += c;
-  c = (uint32_t)(d3 >> 26); h[3] = (uint32_t)d3 & M26; d4 += c;
-  c = (uint32_t)(d4 >> 26); h[4] = (uint32_t)d4 & M26;
+  const uint32_t h0 = h[0], h1 = h[1], h2 = h[2], h3 = h[3], h4 = h[4];
+  uint64_t d = (uint64_t)h0 * r[0] + (uint64_t)h1 * s[4] + (uint64_t)h2 * s[3] + (uint64_t)h3 * s[2] +
+               (uint64_t)h4 * s[1];
+  h[0] = (uint32_t)d & M26;
+  d = (uint64_t)(uint32_t)(d >> 26) + (uint64_t)h0 * r[1] + (uint64_t)h1 * r[0] + (uint64_t)h2 * s[4] +
+      (uint64_t)h3 * s[3] + (uint64_t)h4 * s[2];
+  h[1] = (uint32_t)d & M26;
+  d = (uint64_t)(uint32_t)(d >> 26) + (uint64_t)h0 * r[2] + (uint64_t)h1 * r[1] + (uint64_t)h2 * r[0] +
+      (uint64_t)h3 * s[4] + (uint64_t)h4 * s[3];
+  h[2] = (uint32_t)d & M26;
+  d = (uint64_t)(uint32_t)(d >> 26) + (uint64_t)h0 * r[3] + (uint64_t)h1 * r[2] + (uint64_t)h2 * r[1] +
+      (uint64_t)h3 * r[0] + (uint64_t)h4 * s[4];
+  h[3] = (uint32_t)d & M26;
+  d = (uint64_t)(uint32_t)(d >> 26) + (uint64_t)h0 * r[4] + (uint64_t)h1 * r[3] + (uint64_t)h2 * r[2] +
+      (uint64_t)h3 * r[1] + (uint64_t)h4 * r[0];
+  h[4] = (uint32_t)d & M26;
+  uint32_t c = (uint32_t)(d >> 26);
   h[0] += c * 5u;
   c = h[0] >> 26; h[0] &= M26;
   h[1] += c;

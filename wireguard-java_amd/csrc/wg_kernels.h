@@ -31,6 +31,7 @@ struct TileParams {
   const uint32_t* ntiles_dev;  // non-uniform: tile count computed on device
   uint32_t max_tile_pkts;      // LDS sizing of the per-packet records
   uint32_t poly_g;             // lanes per packet in the Poly1305 phase
+  uint64_t* stamps;            // diagnostic build only (WG_DIAG): per-tile phase timestamps
 };
 
 template <int MODE, bool GENERAL>
@@ -40,10 +41,11 @@ __global__ void k_plan_count(const void* desc, uint32_t n, uint32_t max_len, uin
 __global__ void k_plan_tiles(const uint32_t* prefix, uint32_t n, uint32_t C, uint32_t* tile_start, uint32_t* ntiles,
                              uint32_t max_tiles);
 
-// LDS bytes of the per-packet records of a tile holding up to `mp` packets;
-// the payload image follows, 16-byte aligned (see TileLds in wg_kernels.hip).
+// LDS bytes of the per-packet records of a tile holding up to `mp` packets
+// (128-byte record + 4-byte first-block index each, plus one); the payload
+// image follows, 16-byte aligned (see tile_rec in wg_kernels.hip).
 __host__ __device__ inline uint32_t tile_header_bytes(uint32_t mp) {
-  uint32_t b = 3u * 8u * mp + 4u * ((mp + 1) + 5u * mp + 8u * mp + 4u * mp + 8u * mp);
+  uint32_t b = 128u * mp + 4u * (mp + 1);
   return (b + 15u) & ~15u;
 }
 

@@ -26,6 +26,21 @@ namespace wgk {
 
 using namespace wgd;
 
+// In-kernel phase stamps, compiled only into the diagnostic library
+// (make diag -> libwgaead_diag.so); the product build has none.
+#ifdef WG_DIAG
+#define WG_STAMP(i)                                                                      \
+  do {                                                                                   \
+    if (P.stamps && threadIdx.x == 0) {                                                  \
+      uint64_t t_;                                                                       \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");           \
+      P.stamps[(size_t)blockIdx.x * 8 + (i)] = t_;                                       \
+    }                                                                                    \
+  } while (0)
+#else
+#define WG_STAMP(i) do {} while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // descriptors
 struct Pkt {
@@ -64,38 +79,75 @@ __device__ __forceinline__ uint32_t pkt_blocks(uint32_t len) {
 
 // ---------------------------------------------------------------------------
 // 64-byte block IO. Fast path: whole, 16-byte aligned block -> 4 x dwordx4.
-// Slow path (packet tails, unaligned packets): predicated byte accesses.
+// Partial blocks (packet tails) and unaligned packets go chunk by chunk:
+// whole 16-byte chunks still use dwordx4 when aligned, the remainder uses
+// dword accesses when 4-byte aligned and byte accesses otherwise.
+__device__ __forceinline__ uint32_t ld_bytes(const uint8_t* p, int n) {
+  uint32_t v = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+    if (b < n) v |= (uint32_t)p[b] << (8 * b);
+  return v;
+}
+
 __device__ __forceinline__ void load_block(const uint8_t* src, uint32_t n, uint32_t w[16]) {
-  if (n == 64u && (((uintptr_t)src) & 15u) == 0) {
+  const uintptr_t a = (uintptr_t)src;
+  if (n == 64u && (a & 15u) == 0) {
     const uint4* p = (const uint4*)src;
-    uint4 a = p[0], b = p[1], c = p[2], d = p[3];
-    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
-    w[8] = c.x; w[9] = c.y; w[10] = c.z; w[11] = c.w; w[12] = d.x; w[13] = d.y; w[14] = d.z; w[15] = d.w;
-  } else {
+    uint4 x0 = p[0], x1 = p[1], x2 = p[2], x3 = p[3];
+    w[0] = x0.x; w[1] = x0.y; w[2] = x0.z; w[3] = x0.w; w[4] = x1.x; w[5] = x1.y; w[6] = x1.z; w[7] = x1.w;
+    w[8] = x2.x; w[9] = x2.y; w[10] = x2.z; w[11] = x2.w; w[12] = x3.x; w[13] = x3.y; w[14] = x3.z; w[15] = x3.w;
+    return;
+  }
+  const bool a4 = (a & 3u) == 0, a16 = (a & 15u) == 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      uint32_t v = 0;
+  for (int c = 0; c < 4; ++c) {
+    const int rem = (int)n - 16 * c;
+    if (rem >= 16 && a16) {
+      uint4 x = ((const uint4*)src)[c];
+      w[4 * c] = x.x; w[4 * c + 1] = x.y; w[4 * c + 2] = x.z; w[4 * c + 3] = x.w;
+    } else {
 #pragma unroll
-      for (int b = 0; b < 4; ++b)
-        if ((uint32_t)(4 * k + b) < n) v |= (uint32_t)src[4 * k + b] << (8 * b);
-      w[k] = v;
+      for (int k = 0; k < 4; ++k) {
+        const int r = rem - 4 * k;
+        const uint8_t* q = src + 16 * c + 4 * k;
+        w[4 * c + k] = r <= 0 ? 0u : (r >= 4 && a4) ? *(const uint32_t*)q : ld_bytes(q, r);
+      }
     }
   }
 }
 
+__device__ __forceinline__ void st_bytes(uint8_t* p, uint32_t v, int n) {
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+    if (b < n) p[b] = (uint8_t)(v >> (8 * b));
+}
+
 __device__ __forceinline__ void store_block(uint8_t* dst, uint32_t n, const uint32_t w[16]) {
-  if (n == 64u && (((uintptr_t)dst) & 15u) == 0) {
+  const uintptr_t a = (uintptr_t)dst;
+  if (n == 64u && (a & 15u) == 0) {
     uint4* p = (uint4*)dst;
     p[0] = make_uint4(w[0], w[1], w[2], w[3]);
     p[1] = make_uint4(w[4], w[5], w[6], w[7]);
     p[2] = make_uint4(w[8], w[9], w[10], w[11]);
     p[3] = make_uint4(w[12], w[13], w[14], w[15]);
-  } else {
+    return;
+  }
+  const bool a4 = (a & 3u) == 0, a16 = (a & 15u) == 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k)
+  for (int c = 0; c < 4; ++c) {
+    const int rem = (int)n - 16 * c;
+    if (rem >= 16 && a16) {
+      ((uint4*)dst)[c] = make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
+    } else {
 #pragma unroll
-      for (int b = 0; b < 4; ++b)
-        if ((uint32_t)(4 * k + b) < n) dst[4 * k + b] = (uint8_t)(w[k] >> (8 * b));
+      for (int k = 0; k < 4; ++k) {
+        const int r = rem - 4 * k;
+        uint8_t* q = dst + 16 * c + 4 * k;
+        if (r >= 4 && a4) *(uint32_t*)q = w[4 * c + k];
+        else if (r > 0) st_bytes(q, w[4 * c + k], r);
+      }
+    }
   }
 }
 
@@ -139,43 +191,27 @@ __device__ __forceinline__ void load_chunk16(const uint8_t* src, uint32_t n, uin
 }
 
 // ---------------------------------------------------------------------------
-// LDS tile header: per-packet records (struct of arrays) followed by the image.
-struct TileLds {
-  uint32_t* blk;     // [mp + 1] tile-local first block of packet q
-  uint32_t* len;     // [mp]
-  uint32_t* aadlen;  // [mp]
-  uint32_t* flags;   // [mp] bit0 = valid
-  uint32_t* key;     // [mp * 8] ChaCha key (AEAD/CIPHER) or one-time key (MAC)
-  uint32_t* nonce;   // [mp * 4] n0, n1, n2, ctr0
-  uint32_t* otk;     // [mp * 8] Poly1305 one-time key from block 0
-  uint32_t* verdict; // [mp]
-  uint64_t* in_off;  // [mp]
-  uint64_t* out_off; // [mp]
-  uint64_t* aad_off; // [mp]
-  uint8_t* img;      // image bytes
-};
-
-__device__ __forceinline__ TileLds carve(uint8_t* base, uint32_t mp) {
-  TileLds t;
-  t.in_off = (uint64_t*)base;
-  t.out_off = t.in_off + mp;
-  t.aad_off = t.out_off + mp;
-  uint32_t* u = (uint32_t*)(t.aad_off + mp);
-  t.blk = u; u += mp + 1;
-  t.len = u; u += mp;
-  t.aadlen = u; u += mp;
-  t.flags = u; u += mp;
-  t.verdict = u; u += mp;
-  t.key = u; u += 8 * mp;
-  t.nonce = u; u += 4 * mp;
-  t.otk = u; u += 8 * mp;
-  t.img = base + tile_header_bytes(mp);
-  return t;
-}
+// LDS tile: per-packet records (128 bytes each, read as 16-byte vectors) then the
+// payload image (MAC input, 64-byte granules, zero padded to 16 per packet).
+//   rec[q * 8 + 0] = {in_off lo, in_off hi, out_off lo, out_off hi}
+//   rec[q * 8 + 1] = {len, valid, first tile block, aad_len}
+//   rec[q * 8 + 2] = {aad_off lo, aad_off hi, verdict, image byte offset}
+//   rec[q * 8 + 3] = {n0, n1, n2, ctr0}          nonce words, CIPHER start counter
+//   rec[q * 8 + 4..5] = key (ChaCha key, or the MAC one-time key)
+//   rec[q * 8 + 6..7] = Poly1305 one-time key from block 0 (AEAD)
+// blk[q] (u32, mp + 1 entries) duplicates the first-block column for the search.
+__device__ __forceinline__ uint4* tile_rec(uint8_t* base) { return (uint4*)base; }
+__device__ __forceinline__ uint32_t* tile_blk(uint8_t* base, uint32_t mp) { return (uint32_t*)(base + 128u * mp); }
+__device__ __forceinline__ uint8_t* tile_img(uint8_t* base, uint32_t mp) { return base + tile_header_bytes(mp); }
 
 __device__ __forceinline__ void shfl5(const uint32_t v[5], int src, uint32_t o[5]) {
 #pragma unroll
   for (int i = 0; i < 5; ++i) o[i] = __shfl(v[i], src, 64);
+}
+
+__device__ __forceinline__ void lds_load_chunk(const uint8_t* p, uint32_t w[4]) {
+  uint4 v = *(const uint4*)p;
+  w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
 }
 
 // ---------------------------------------------------------------------------
@@ -185,6 +221,14 @@ __global__ void __launch_bounds__(WG_TPB) k_tile(TileParams P) {
   constexpr bool AEAD = (MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN);
   const uint32_t tid = threadIdx.x;
   const uint32_t tile = blockIdx.x;
+  WG_STAMP(0);
+#ifdef WG_DIAG
+  if (P.stamps && tid == 0) {
+    P.stamps[(size_t)blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memrealtime();
+    P.stamps[(size_t)blockIdx.x * 8 + 6] = __builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_ID
+    P.stamps[(size_t)blockIdx.x * 8 + 7] = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // XCC_ID
+  }
+#endif
 
   uint32_t p0, p1;
   if (P.uniform) {
@@ -197,41 +241,42 @@ __global__ void __launch_bounds__(WG_TPB) k_tile(TileParams P) {
     p1 = P.tile_start[tile + 1];
   }
   const uint32_t np = p1 - p0;
-  TileLds L = carve(lds_raw, P.max_tile_pkts);
+  const uint32_t mp = P.max_tile_pkts;
+  uint4* rec = tile_rec(lds_raw);
+  uint32_t* blk = tile_blk(lds_raw, mp);
+  uint8_t* img_base = tile_img(lds_raw, mp);
 
   // ---- packet records --------------------------------------------------------
   for (uint32_t q = tid; q < np; q += WG_TPB) {
     Pkt pk = load_pkt<GENERAL>(P.desc, p0 + q);
-    uint32_t len = pk.len;
+    const uint32_t len = pk.len;
     bool ok = len <= P.max_len && pk.key_slot < P.key_slots;
     if (P.uniform) ok = ok && len == P.max_len;
-    // bounds against the caller's buffers
-    uint64_t in_need = (uint64_t)len + (MODE == WG_MODE_OPEN ? 16u : 0u);
-    uint64_t out_need = (uint64_t)len + (MODE == WG_MODE_SEAL ? 16u : 0u);
-    if (MODE == WG_MODE_MAC) out_need = 16u;
+    const uint64_t in_need = (uint64_t)len + (MODE == WG_MODE_OPEN ? 16u : 0u);
+    const uint64_t out_need = MODE == WG_MODE_MAC ? 16u : (uint64_t)len + (MODE == WG_MODE_SEAL ? 16u : 0u);
     ok = ok && pk.in_off <= P.in_size && in_need <= P.in_size - pk.in_off;
     ok = ok && pk.out_off <= P.out_size && out_need <= P.out_size - pk.out_off;
     if (GENERAL && AEAD && pk.aad_len)
       ok = ok && pk.aad_off <= P.aad_size && (uint64_t)pk.aad_len <= P.aad_size - pk.aad_off;
-    L.len[q] = len;
-    L.aadlen[q] = pk.aad_len;
-    L.flags[q] = ok ? 1u : 0u;
-    L.verdict[q] = 0u;
-    L.in_off[q] = pk.in_off;
-    L.out_off[q] = pk.out_off;
-    L.aad_off[q] = pk.aad_off;
-    L.nonce[4 * q + 0] = pk.n0; L.nonce[4 * q + 1] = pk.n1; L.nonce[4 * q + 2] = pk.n2; L.nonce[4 * q + 3] = pk.ctr0;
+    const uint32_t b0 = P.uniform ? q * P.nb_uniform : P.blk_prefix[p0 + q] - P.blk_prefix[p0];
+    blk[q] = b0;
+    const uint32_t img_off = 64u * (b0 - (AEAD ? q : 0u));
+    uint4* r = rec + 8u * q;
+    r[0] = make_uint4((uint32_t)pk.in_off, (uint32_t)(pk.in_off >> 32), (uint32_t)pk.out_off,
+                      (uint32_t)(pk.out_off >> 32));
+    r[1] = make_uint4(len, ok ? 1u : 0u, b0, pk.aad_len);
+    r[2] = make_uint4((uint32_t)pk.aad_off, (uint32_t)(pk.aad_off >> 32), 0u, img_off);
+    r[3] = make_uint4(pk.n0, pk.n1, pk.n2, pk.ctr0);
     const uint4* kp = (const uint4*)(P.keys + 8u * (ok ? pk.key_slot : 0u));
-    uint4 ka = kp[0], kb = kp[1];
-    uint32_t* kd = L.key + 8 * q;
-    kd[0] = ka.x; kd[1] = ka.y; kd[2] = ka.z; kd[3] = ka.w; kd[4] = kb.x; kd[5] = kb.y; kd[6] = kb.z; kd[7] = kb.w;
-    L.blk[q] = P.uniform ? q * P.nb_uniform : P.blk_prefix[p0 + q] - P.blk_prefix[p0];
+    r[4] = kp[0];
+    r[5] = kp[1];
   }
-  if (tid == 0) L.blk[np] = P.uniform ? np * P.nb_uniform : P.blk_prefix[p1] - P.blk_prefix[p0];
+  if (tid == 0) blk[np] = P.uniform ? np * P.nb_uniform : P.blk_prefix[p1] - P.blk_prefix[p0];
   __syncthreads();
+  WG_STAMP(1);
 
   // ---- phase 1: ChaCha20 over every counter block of the tile ---------------
-  const uint32_t nblk = L.blk[np];
+  const uint32_t nblk = blk[np];
   for (uint32_t b = tid; b < nblk; b += WG_TPB) {
     uint32_t q;
     if (P.uniform) {
@@ -239,126 +284,124 @@ __global__ void __launch_bounds__(WG_TPB) k_tile(TileParams P) {
     } else {  // last q with blk[q] <= b
       uint32_t lo = 0, hi = np;
       while (hi - lo > 1) {
-        uint32_t mid = (lo + hi) >> 1;
-        if (L.blk[mid] <= b) lo = mid; else hi = mid;
+        const uint32_t mid = (lo + hi) >> 1;
+        if (blk[mid] <= b) lo = mid; else hi = mid;
       }
       q = lo;
     }
-    if (!(L.flags[q] & 1u)) continue;
-    const uint32_t j = b - L.blk[q];
-    const uint32_t len = L.len[q];
-    const uint32_t d = AEAD ? j - 1u : j;  // data block index
-    uint8_t* img = L.img + 64u * (L.blk[q] - (AEAD ? q : 0u));
+    const uint4* r = rec + 8u * q;
+    const uint4 r1 = r[1];
+    if (!r1.y) continue;
+    const uint32_t len = r1.x, j = b - r1.z;
+    const uint32_t d = AEAD ? j - 1u : j;  // data block index (AEAD block 0 = Poly1305 key)
+    const bool data = !(AEAD && j == 0);
+    const uint4 r0 = r[0];
+    const uint64_t in_off = (uint64_t)r0.x | ((uint64_t)r0.y << 32);
+    const uint64_t out_off = (uint64_t)r0.z | ((uint64_t)r0.w << 32);
+    const uint32_t off = 64u * d;
+    const uint32_t n = data ? min(64u, len - off) : 0u;
+    uint8_t* img = img_base + r[2].w + off;
+    uint32_t w[16];
+    if (data) load_block(P.in + in_off + off, n, w);  // in flight during the rounds below
 
     if constexpr (MODE == WG_MODE_MAC) {
-      uint32_t off = 64u * d, n = min(64u, len - off);
-      uint32_t w[16];
-      load_block(P.in + L.in_off[q] + off, n, w);
-      mask_block(n, w);
-      lds_store_block(img + off, w);
-      continue;
+      if (n < 64u) mask_block(n, w);
+      lds_store_block(img, w);
     } else {
-      uint32_t key[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) key[i] = L.key[8 * q + i];
-      const uint32_t n0 = L.nonce[4 * q + 0], n1 = L.nonce[4 * q + 1], n2 = L.nonce[4 * q + 2];
-      const uint32_t ctr = (MODE == WG_MODE_CIPHER) ? L.nonce[4 * q + 3] + j : j;
+      const uint4 ka = r[4], kb = r[5], nn = r[3];
+      const uint32_t key[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
+      const uint32_t ctr = (MODE == WG_MODE_CIPHER) ? nn.w + j : j;
       uint32_t ks[16];
-      chacha20_block(key, ctr, n0, n1, n2, ks);
-      if (AEAD && j == 0) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) L.otk[8 * q + i] = ks[i];
+      chacha20_block(key, ctr, nn.x, nn.y, nn.z, ks);
+      if (!data) {
+        uint4* o = (uint4*)(rec + 8u * q + 6);
+        o[0] = make_uint4(ks[0], ks[1], ks[2], ks[3]);
+        o[1] = make_uint4(ks[4], ks[5], ks[6], ks[7]);
         continue;
       }
-      const uint32_t off = 64u * d, n = min(64u, len - off);
-      uint32_t w[16];
-      load_block(P.in + L.in_off[q] + off, n, w);
       if constexpr (MODE == WG_MODE_OPEN) {
-        mask_block(n, w);
-        lds_store_block(img + off, w);  // MAC over the received ciphertext
+        if (n < 64u) mask_block(n, w);
+        lds_store_block(img, w);  // MAC over the received ciphertext
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) w[i] ^= ks[i];
-      store_block(P.out + L.out_off[q] + off, n, w);
+      store_block(P.out + out_off + off, n, w);
       if constexpr (MODE == WG_MODE_SEAL) {
-        mask_block(n, w);
-        lds_store_block(img + off, w);  // MAC over the ciphertext just produced
+        if (n < 64u) mask_block(n, w);
+        lds_store_block(img, w);  // MAC over the ciphertext just produced
       }
     }
   }
-  if constexpr (MODE == WG_MODE_CIPHER) return;
+  if constexpr (MODE == WG_MODE_CIPHER) {
+    WG_STAMP(2);
+    return;
+  }
   __syncthreads();
+  WG_STAMP(2);
 
   // ---- phase 2: Poly1305, G lanes per packet --------------------------------
   {
     const uint32_t G = P.poly_g;
-    const uint32_t ppw = 64u / G;           // packets per wave
+    const uint32_t ppw = 64u / G;  // packets per wave
     const uint32_t lane = tid & 63u, wave = tid >> 6;
     const uint32_t gq = lane / G, j = lane - gq * G;
-    const uint32_t base = gq * G;           // first lane of the group
+    const uint32_t base = gq * G;  // first lane of the group
     const bool lane_used = gq < ppw;
     for (uint32_t qb = wave * ppw; qb < np; qb += (WG_TPB / 64u) * ppw) {
       const uint32_t q = qb + gq;
-      const bool act = lane_used && q < np && (L.flags[q] & 1u);
-      // r, s from the one-time key
-      uint32_t k0, k1, k2, k3, s0, s1, s2, s3;
-      {
-        const uint32_t* src = AEAD ? L.otk : L.key;
-        uint32_t qq = act ? q : 0u;
-        k0 = src[8 * qq + 0]; k1 = src[8 * qq + 1]; k2 = src[8 * qq + 2]; k3 = src[8 * qq + 3];
-        s0 = src[8 * qq + 4]; s1 = src[8 * qq + 5]; s2 = src[8 * qq + 6]; s3 = src[8 * qq + 7];
-      }
-      uint32_t r[5], rs[5];
-      poly_r_limbs(k0, k1, k2, k3, r);
-      // powers: lane j of the group ends with r^(j+1)
-      uint32_t x[5] = {r[0], r[1], r[2], r[3], r[4]};
+      const uint32_t qq = (lane_used && q < np) ? q : 0u;
+      const uint4* r = rec + 8u * qq;
+      const uint4 r1 = r[1];
+      const bool act = lane_used && q < np && r1.y;
+      const uint4 ka = AEAD ? r[6] : r[4];  // r || s
+      const uint4 kb = AEAD ? r[7] : r[5];
+      uint32_t rl[5];
+      poly_r_limbs(ka.x, ka.y, ka.z, ka.w, rl);
+      // powers: lane j of the group ends with r^(j+1) (Hillis-Steele product scan)
+      uint32_t x[5] = {rl[0], rl[1], rl[2], rl[3], rl[4]};
       for (uint32_t st = 1; st < G; st <<= 1) {
         uint32_t y[5], ys[5];
         shfl5(x, (int)(lane >= st ? lane - st : lane), y);
         poly_scale5(y, ys);
         if (j >= st) poly_mul(x, y, ys);
       }
-      uint32_t R[5], Rs[5], W[5], Ws[5];
-      shfl5(x, (int)min(base + G - 1u, 63u), R);
-      shfl5(x, (int)min(base + G - 1u - j, 63u), W);
+      uint32_t R[5], Rs[5];
+      shfl5(x, (int)min(base + G - 1u, 63u), R);  // r^G
       poly_scale5(R, Rs);
-      poly_scale5(W, Ws);
-      (void)rs;
 
       uint32_t acc[5] = {0, 0, 0, 0, 0};
       if (act) {
-        const uint32_t len = L.len[q], alen = L.aadlen[q];
+        const uint32_t len = r1.x, alen = r1.w;
+        const uint4 r2 = r[2];
+        const uint8_t* img = img_base + r2.w;
         const uint32_t na = (alen + 15u) >> 4, nc = (len + 15u) >> 4;
         const uint32_t M = (MODE == WG_MODE_MAC) ? nc : na + nc + 1u;
         const uint32_t K = (M + G - 1u) / G;
         const int D = (int)(K * G - M);
-        const uint8_t* img = L.img + 64u * (L.blk[q] - (AEAD ? q : 0u));
         for (uint32_t k = 0; k < K; ++k) {
           if (k) poly_mul(acc, R, Rs);
           const int t = (int)(j + k * G) - D;
           if (t < 0) continue;
+          const uint32_t tt = (uint32_t)t;
           uint32_t w[4];
           uint32_t hib = 1u << 24;
-          const uint32_t tt = (uint32_t)t;
-          if (MODE == WG_MODE_MAC) {
-            uint4 v = *(const uint4*)(img + 16u * tt);
-            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+          if constexpr (MODE == WG_MODE_MAC) {
+            lds_load_chunk(img + 16u * tt, w);
             const uint32_t rem = len - 16u * tt;
             if (rem < 16u) {  // final partial block: 0x01 pad, no 2^128 bit (poly1305-donna-64.h:162-168)
               hib = 0;
-              const uint32_t sh = 8u * (rem & 3u);
-              const uint32_t wi = rem >> 2;
+              const uint32_t sh = 8u * (rem & 3u), wi = rem >> 2;
               w[0] |= (wi == 0) ? (1u << sh) : 0u;
               w[1] |= (wi == 1) ? (1u << sh) : 0u;
               w[2] |= (wi == 2) ? (1u << sh) : 0u;
               w[3] |= (wi == 3) ? (1u << sh) : 0u;
             }
-          } else if (tt < na) {
+          } else if (GENERAL && tt < na) {
             const uint32_t o = 16u * tt;
-            load_chunk16(P.aad + L.aad_off[q] + o, min(16u, alen - o), w);
+            const uint64_t aad_off = (uint64_t)r2.x | ((uint64_t)r2.y << 32);
+            load_chunk16(P.aad + aad_off + o, min(16u, alen - o), w);
           } else if (tt < na + nc) {
-            uint4 v = *(const uint4*)(img + 16u * (tt - na));
-            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+            lds_load_chunk(img + 16u * (tt - na), w);
           } else {  // le64(aad_len) || le64(ct_len) (ChaCha20Poly1305.java:88-90)
             w[0] = alen; w[1] = 0; w[2] = len; w[3] = 0;
           }
@@ -367,7 +410,13 @@ __global__ void __launch_bounds__(WG_TPB) k_tile(TileParams P) {
 #pragma unroll
           for (int i = 0; i < 5; ++i) acc[i] += c[i];
         }
-        poly_mul(acc, W, Ws);
+      }
+      // scale lane j's partial by r^(G-j) (lane G-1-j holds it after the scan)
+      {
+        uint32_t W[5], Ws[5];
+        shfl5(x, (int)min(base + G - 1u - j, 63u), W);
+        poly_scale5(W, Ws);
+        if (act) poly_mul(acc, W, Ws);
       }
       // group sum into lane j == 0
       for (uint32_t st = 1; st < G; st <<= 1) {
@@ -380,37 +429,49 @@ __global__ void __launch_bounds__(WG_TPB) k_tile(TileParams P) {
       }
       if (act && j == 0) {
         uint32_t tag[4];
-        poly_finish(acc, s0, s1, s2, s3, tag);
-        const uint32_t len = L.len[q];
-        if constexpr (MODE == WG_MODE_SEAL) {
-          uint8_t* tp = P.out + L.out_off[q] + len;
+        poly_finish(acc, kb.x, kb.y, kb.z, kb.w, tag);
+        const uint4 r0 = r[0];
+        const uint64_t in_off = (uint64_t)r0.x | ((uint64_t)r0.y << 32);
+        const uint64_t out_off = (uint64_t)r0.z | ((uint64_t)r0.w << 32);
+        const uint32_t len = r1.x;
+        if constexpr (MODE == WG_MODE_SEAL || MODE == WG_MODE_MAC) {
+          uint8_t* tp = P.out + out_off + (MODE == WG_MODE_SEAL ? len : 0u);
+          if ((((uintptr_t)tp) & 15u) == 0) {
+            *(uint4*)tp = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+          } else {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) store_u32_any(tp + 4 * i, tag[i]);
-        } else if constexpr (MODE == WG_MODE_MAC) {
-          uint8_t* tp = P.out + L.out_off[q];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) store_u32_any(tp + 4 * i, tag[i]);
-        } else {  // OPEN: compare (full 16 bytes, no early exit)
-          const uint8_t* tp = P.in + L.in_off[q] + len;
+            for (int i = 0; i < 4; ++i) store_u32_any(tp + 4 * i, tag[i]);
+          }
+        } else {  // OPEN: compare all 16 bytes, no early exit
+          const uint8_t* tp = P.in + in_off + len;
           uint32_t diff = 0;
 #pragma unroll
           for (int i = 0; i < 4; ++i) diff |= load_u32_any(tp + 4 * i) ^ tag[i];
-          L.verdict[q] = diff ? 1u : 0u;
+          ((uint32_t*)(rec + 8u * q + 2))[2] = diff ? 1u : 0u;
         }
       }
     }
   }
 
+  WG_STAMP(3);
+#ifdef WG_DIAG
+  if (P.stamps && tid == 0) P.stamps[(size_t)blockIdx.x * 8 + 4] = __builtin_amdgcn_s_memrealtime();
+#endif
   if constexpr (MODE == WG_MODE_OPEN) {
     __syncthreads();
+    for (uint32_t q = tid; q < np; q += WG_TPB) {
+      const uint4 r1 = rec[8u * q + 1];
+      const uint32_t bad = r1.y ? ((const uint32_t*)(rec + 8u * q + 2))[2] : 1u;
+      if (P.status) P.status[p0 + q] = bad ? WG_PKT_BADTAG : WG_PKT_OK;
+      if (bad && r1.y) ((uint32_t*)(rec + 8u * q + 2))[2] = 2u;  // needs scrubbing
+    }
+    __syncthreads();
     for (uint32_t q = 0; q < np; ++q) {
-      const bool valid = L.flags[q] & 1u;
-      const uint32_t bad = valid ? L.verdict[q] : 1u;
-      if (tid == 0 && P.status) P.status[p0 + q] = bad ? WG_PKT_BADTAG : WG_PKT_OK;
-      if (bad && valid) {  // scrub the unauthenticated plaintext
-        uint8_t* o = P.out + L.out_off[q];
-        for (uint32_t i = tid; i < L.len[q]; i += WG_TPB) o[i] = 0;
-      }
+      if (((const uint32_t*)(rec + 8u * q + 2))[2] != 2u) continue;
+      const uint4 r0 = rec[8u * q];
+      uint8_t* o = P.out + ((uint64_t)r0.z | ((uint64_t)r0.w << 32));
+      const uint32_t len = rec[8u * q + 1].x;
+      for (uint32_t i = tid; i < len; i += WG_TPB) o[i] = 0;  // scrub unauthenticated plaintext
     }
   }
 }
@@ -447,6 +508,238 @@ __global__ void k_plan_tiles(const uint32_t* prefix, uint32_t n, uint32_t C, uin
   tile_start[t] = (t == T) ? n : lo;
 }
 
+// ---------------------------------------------------------------------------
+// k_stream — transport seal/open, one wave per workgroup, no barriers between waves.
+//
+// The wave is 8 SLOTS of 8 lanes. A slot streams one packet at a time, 512 bytes
+// (8 ChaCha20 counter blocks) per ROUND:
+//   1. lane j of the slot computes counter block 8*round + j (block 0 = the
+//      Poly1305 key block, ChaCha20Poly1305.java:11-14; block b >= 1 = payload
+//      bytes 64(b-1).., ChaCha20Poly1305.java:36) with its 64 payload bytes
+//      prefetched before the rounds, XORs, stores, and leaves the MAC input
+//      (ciphertext) of the round in a 4 KB LDS image;
+//   2. the same 8 lanes advance an 8-strided Horner evaluation of the MAC
+//      polynomial over the round's 16-byte chunks: lane j owns the message
+//      positions congruent to j mod 8 (leading zero padding D = 8K - M aligns the
+//      last position to lane 7) and multiplies by R = r^8 per position.
+// On the packet's last round each lane scales its partial by r^(8-j), the slot
+// sums its 8 partials with shuffles and lane 0 finishes the tag
+// (ChaCha20Poly1305.java:63-93). Finished slots take the wave's next packet, so
+// mixed lengths keep every slot busy. Register/LDS budget: ~5 KB LDS per wave,
+// so a CU holds up to 32 waves.
+constexpr uint32_t SLOT_LANES = 8;
+
+struct StreamParams {
+  const wg_pkt* desc;
+  uint32_t n;
+  uint32_t ppw;  // packets per wave (consecutive descriptors)
+  uint32_t max_len;
+  uint32_t key_slots;
+  const uint8_t* in;
+  uint64_t in_size;
+  uint8_t* out;
+  uint64_t out_size;
+  const uint32_t* keys;
+  uint32_t* status;
+};
+
+template <int MODE>
+__global__ void __launch_bounds__(64) k_stream(StreamParams P) {
+  static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
+  __shared__ uint4 img[8 * 8 * 4];  // [slot][lane][4 chunks]: the round's MAC input
+  __shared__ uint4 skey[8 * 2];     // per-slot ChaCha key
+  __shared__ uint4 sotk[8 * 2];     // per-slot Poly1305 one-time key (r || s)
+  __shared__ uint32_t spow[8 * 10]; // per-slot R = r^8 limbs and 5R (limbs 1..4)
+  __shared__ uint32_t lpow[64 * 5]; // per-lane W = r^(8-j) limbs
+  const uint32_t lane = threadIdx.x, s = lane >> 3, j = lane & 7u;
+  const uint32_t sbase = lane & ~7u;
+  const uint32_t w0 = blockIdx.x * P.ppw, w1 = min(P.n, w0 + P.ppw);
+  uint32_t next = w0 + SLOT_LANES;  // wave-uniform
+  uint32_t pkt = w0 + s;
+  bool have = pkt < w1;
+  uint32_t round = 0;
+  // packet state (identical in the 8 lanes of a slot)
+  uint64_t in_off = 0, out_off = 0;
+  uint32_t len = 0, ctr_lo = 0, ctr_hi = 0, nb = 0, nc = 0, D = 0;
+  bool valid = false;
+  uint32_t acc[5];
+
+  while (__any(have)) {
+    if (have && round == 0) {  // start a packet: descriptor, bounds, key
+      const uint4* dp = (const uint4*)(P.desc + pkt);
+      const uint4 lo = dp[0], hi = dp[1];
+      in_off = (uint64_t)lo.x | ((uint64_t)lo.y << 32);
+      out_off = (uint64_t)lo.z | ((uint64_t)lo.w << 32);
+      ctr_lo = hi.x; ctr_hi = hi.y; len = hi.z;
+      const uint32_t ks_ = hi.w;
+      valid = len <= P.max_len && ks_ < P.key_slots;
+      const uint64_t in_need = (uint64_t)len + (MODE == WG_MODE_OPEN ? 16u : 0u);
+      const uint64_t out_need = (uint64_t)len + (MODE == WG_MODE_SEAL ? 16u : 0u);
+      valid = valid && in_off <= P.in_size && in_need <= P.in_size - in_off;
+      valid = valid && out_off <= P.out_size && out_need <= P.out_size - out_off;
+      nb = ((len + 63u) >> 6) + 1u;
+      nc = (len + 15u) >> 4;
+      const uint32_t M = nc + 1u, K = (M + 7u) >> 3;
+      D = 8u * K - M;
+      acc[0] = acc[1] = acc[2] = acc[3] = acc[4] = 0;
+      if (j == 0 && valid) {
+        const uint4* kp = (const uint4*)(P.keys + 8u * ks_);
+        skey[2 * s] = kp[0];
+        skey[2 * s + 1] = kp[1];
+      }
+    }
+    __syncthreads();  // one wave per workgroup: orders the slot key writes
+
+    // ---- ChaCha20: block b of the slot's packet ------------------------------------
+    const uint32_t b = 8u * round + j;
+    const bool act = have && valid && b < nb;
+    const bool data = act && b > 0;
+    const uint32_t off = 64u * (b - 1u);
+    const uint32_t nbytes = data ? min(64u, len - off) : 0u;
+    uint32_t w[16];
+    if (data) load_block(P.in + in_off + off, nbytes, w);  // in flight during the rounds
+    if (act) {
+      const uint4 ka = skey[2 * s], kb = skey[2 * s + 1];
+      const uint32_t key[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
+      uint32_t ks[16];
+      chacha20_block(key, b, ctr_lo, ctr_hi, 0u, ks);
+      if (!data) {
+        sotk[2 * s] = make_uint4(ks[0], ks[1], ks[2], ks[3]);
+        sotk[2 * s + 1] = make_uint4(ks[4], ks[5], ks[6], ks[7]);
+      } else {
+        if constexpr (MODE == WG_MODE_OPEN) {
+          if (nbytes < 64u) mask_block(nbytes, w);
+          lds_store_block((uint8_t*)&img[4 * lane], w);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] ^= ks[i];
+        store_block(P.out + out_off + off, nbytes, w);
+        if constexpr (MODE == WG_MODE_SEAL) {
+          if (nbytes < 64u) mask_block(nbytes, w);
+          lds_store_block((uint8_t*)&img[4 * lane], w);
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- Poly1305 ------------------------------------------------------------------
+    if (have && valid) {
+      if (round == 0) {  // r and its powers: lane j gets r^(j+1); R = r^8, W = r^(8-j)
+        const uint4 o = sotk[2 * s];
+        uint32_t x[5];
+        poly_r_limbs(o.x, o.y, o.z, o.w, x);
+#pragma unroll
+        for (uint32_t st = 1; st < 8u; st <<= 1) {
+          uint32_t y[5], ys[5];
+          shfl5(x, (int)(j >= st ? lane - st : lane), y);
+          poly_scale5(y, ys);
+          if (j >= st) poly_mul(x, y, ys);
+        }
+        uint32_t R[5], W[5];
+        shfl5(x, (int)(sbase + 7u), R);
+        shfl5(x, (int)(sbase + 7u - j), W);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) lpow[5 * lane + i] = W[i];
+        if (j == 0) {
+#pragma unroll
+          for (int i = 0; i < 5; ++i) spow[10 * s + i] = R[i];
+#pragma unroll
+          for (int i = 1; i < 5; ++i) spow[10 * s + 5 + i] = R[i] * 5u;
+        }
+      }
+      uint32_t R[5], Rs[5];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) R[i] = spow[10 * s + i];
+      Rs[0] = 0;
+#pragma unroll
+      for (int i = 1; i < 5; ++i) Rs[i] = spow[10 * s + 5 + i];
+      // this round's message chunks: data blocks 8r..8r+7 -> chunks [4(8r-1), 4(8r+7)) of [0, nc)
+      const uint32_t blo = max(8u * round, 1u);
+      const uint32_t c_lo = 4u * (blo - 1u);
+      const bool last = 8u * (round + 1u) >= nb;
+      const uint32_t c_end = last ? nc + 1u : min(nc, 4u * (8u * round + 7u));
+      // first chunk c >= c_lo with (c + D) % 8 == j
+      uint32_t c = c_lo + ((j - ((c_lo + D) & 7u)) & 7u);
+      for (; c < c_end; c += 8u) {
+        poly_mul(acc, R, Rs);
+        uint32_t m0, m1, m2, m3;
+        if (c < nc) {
+          const uint32_t blk_lane = (c >> 2) + 1u - 8u * round;  // lane of the slot holding it
+          const uint4 v = img[4u * (sbase + blk_lane) + (c & 3u)];
+          m0 = v.x; m1 = v.y; m2 = v.z; m3 = v.w;
+        } else {  // le64(0) || le64(len): no AAD on the transport path (ChaCha20Poly1305.java:88-90)
+          m0 = 0; m1 = 0; m2 = len; m3 = 0;
+        }
+        uint32_t cl[5];
+        poly_block_limbs(m0, m1, m2, m3, 1u << 24, cl);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) acc[i] += cl[i];
+      }
+    }
+
+    // ---- finish packets whose last round this was ------------------------------------
+    const bool done = have && (!valid || 8u * (round + 1u) >= nb);
+    if (done) {
+      if (valid) {
+        uint32_t W[5], Ws[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) W[i] = lpow[5 * lane + i];
+        poly_scale5(W, Ws);
+        poly_mul(acc, W, Ws);
+#pragma unroll
+        for (uint32_t st = 1; st < 8u; st <<= 1) {
+          uint32_t y[5];
+          shfl5(acc, (int)(j + st < 8u ? lane + st : lane), y);
+          if (j + st < 8u) {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) acc[i] += y[i];
+          }
+        }
+      }
+      uint32_t bad = valid ? 0u : 1u;
+      if (j == 0 && valid) {
+        const uint4 sv = sotk[2 * s + 1];
+        uint32_t tag[4];
+        poly_finish(acc, sv.x, sv.y, sv.z, sv.w, tag);
+        if constexpr (MODE == WG_MODE_SEAL) {
+          uint8_t* tp = P.out + out_off + len;
+          if ((((uintptr_t)tp) & 15u) == 0) {
+            *(uint4*)tp = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) store_u32_any(tp + 4 * i, tag[i]);
+          }
+        } else {  // all 16 bytes compared, no early exit
+          const uint8_t* tp = P.in + in_off + len;
+          uint32_t diff = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) diff |= load_u32_any(tp + 4 * i) ^ tag[i];
+          bad = diff ? 1u : 0u;
+        }
+      }
+      if constexpr (MODE == WG_MODE_OPEN) {
+        bad = __shfl(bad, (int)sbase, 64);
+        if (j == 0 && P.status) P.status[pkt] = bad ? WG_PKT_BADTAG : WG_PKT_OK;
+        if (bad && valid) {  // scrub the unauthenticated plaintext written this call
+          uint8_t* o = P.out + out_off;
+          for (uint32_t i = j; i < len; i += 8u) o[i] = 0;
+        }
+      }
+    }
+    // hand the wave's next packets to the slots that finished (ballot rank)
+    const unsigned long long fin = __ballot(done && j == 0);
+    if (done) {
+      const uint32_t rank = (uint32_t)__popcll(fin & ((1ull << sbase) - 1ull));
+      pkt = next + rank;
+      have = pkt < w1;
+      round = 0;
+    } else if (have) {
+      ++round;
+    }
+    next += (uint32_t)__popcll(fin);
+  }
+}
+
 // explicit instantiations used by wg_capi.hip
 template __global__ void k_tile<WG_MODE_SEAL, false>(TileParams);
 template __global__ void k_tile<WG_MODE_OPEN, false>(TileParams);
@@ -460,5 +753,7 @@ template __global__ void k_plan_count<WG_MODE_SEAL, true>(const void*, uint32_t,
 template __global__ void k_plan_count<WG_MODE_OPEN, true>(const void*, uint32_t, uint32_t, uint32_t*);
 template __global__ void k_plan_count<WG_MODE_CIPHER, true>(const void*, uint32_t, uint32_t, uint32_t*);
 template __global__ void k_plan_count<WG_MODE_MAC, true>(const void*, uint32_t, uint32_t, uint32_t*);
+template __global__ void k_stream<WG_MODE_SEAL>(StreamParams);
+template __global__ void k_stream<WG_MODE_OPEN>(StreamParams);
 
 }  // namespace wgk

@@ -31,9 +31,15 @@ def pack_desc(in_off, out_off, counter, length, key_slot) -> np.ndarray:
     return d
 
 
+WG_AEAD_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("aad_off", "<u8"), ("len", "<u4"),
+                          ("aad_len", "<u4"), ("key_slot", "<u4"), ("ctr0", "<u4"), ("nonce", "<u4", (3,)),
+                          ("_reserved", "<u4", (3,))])
+
+
 def desc_as_int64(d: np.ndarray) -> np.ndarray:
     """wg_pkt array viewed as int64 [n, 4] (for torch.from_numpy)."""
-    return np.ascontiguousarray(d).view(np.int64).reshape(-1, 4)
+    d = np.ascontiguousarray(d)
+    return d.view(np.int64).reshape(-1, d.dtype.itemsize // 8)
 
 
 class Engine:
@@ -103,6 +109,16 @@ class Engine:
         n = desc.shape[0]
         L.check(self._lib.wg_open_batch(self.ctx, desc.data_ptr(), n, inp.data_ptr(), inp.numel(), out.data_ptr(),
                                         out.numel(), status.data_ptr(), max_len, L.WG_F_UNIFORM if uniform else 0,
+                                        stream if stream is not None else _torch_stream()))
+
+    def aead(self, mode: int, desc, inp, aad, out, status, max_len: int, stream: int | None = None):
+        """wg_aead_batch over torch tensors: desc int64 [n, 8] (wg_aead_desc records)."""
+        n = desc.shape[0]
+        L.check(self._lib.wg_aead_batch(self.ctx, mode, desc.data_ptr(), n, inp.data_ptr() if inp is not None else None,
+                                        inp.numel() if inp is not None else 0,
+                                        aad.data_ptr() if aad is not None else None,
+                                        aad.numel() if aad is not None else 0, out.data_ptr(), out.numel(),
+                                        status.data_ptr() if status is not None else None, max_len,
                                         stream if stream is not None else _torch_stream()))
 
     # ---- host buffers ---------------------------------------------------------------
