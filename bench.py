@@ -17,7 +17,7 @@ works on its own shard — no collective on the data path. The only collectives
 are the timing barrier and the max-over-ranks reduction.
 
 The JSON line also carries:
-  roofline      the seal kernel (k_tile<SEAL>) against the 8 TB/s HBM peak, with
+  roofline      the seal kernel (k_stream<SEAL>) against the 8 TB/s HBM peak, with
                 algorithmic bytes = n * (2L + 16) per launch and the launch duration
                 from HIP events on the launch stream; `traffic` from the committed
                 rocprofv3 PMC summary (profiles/pmc_*.json) when present
@@ -246,7 +246,7 @@ def main():
             "data": "synthetic (random payload in HBM, splitmix64 keys, sequential counters)",
             "config": {"workload": wdesc, "packets_per_gpu": n, "payload_bytes": int(lengths.mean()),
                        "sessions_per_gpu": nkeys, "parallelism": f"dp{world} sharded by session, no collective"},
-            "roofline": {"bound": "hbm", "kernel": "k_tile<SEAL>", "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": "k_stream<SEAL>", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "seal_ms": round(seal_ms, 4), "open_ms": round(open_ms, 4),
                          "alg_bytes_per_launch": int(seal_alg)},

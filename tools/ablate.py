@@ -41,6 +41,12 @@ def t(fn, reps=20):
     return a.elapsed_time(b) / reps * 1e3
 
 
+if os.environ.get("ABLATE") == "transport":
+    for name, fn in [("seal", lambda: eng.seal(tdesc, buf, out, L, uniform=True)),
+                     ("open", lambda: eng.open(tdesc, out, buf, st, L, uniform=True))]:
+        print(f"{name:32s} {t(fn, 5):9.2f} us")
+    sys.exit(0)
+
 res = {
     "seal(transport,uniform)": t(lambda: eng.seal(tdesc, buf, out, L, uniform=True)),
     "open(transport,uniform)": t(lambda: eng.open(tdesc, out, buf, st, L, uniform=True)),

@@ -112,10 +112,18 @@ struct Tunables {
   uint32_t tile_passes = 2, poly_waves = 4, poly_gmax = 16;
   uint32_t stream_ppw_uniform = 8, stream_ppw_mixed = 16;  // packets per wave in k_stream
   int use_tile_for_transport = 0;                           // 1: route transport batches to k_tile
+  int stream_variant = 1;                                   // k_stream<MODE, V> variant bits
+  int use_pipe = 0;                                         // k_pipe (software-pipelined) for transport
+  int use_lean = 0;                                         // k_lean (state in LDS) for transport
   Tunables() {
     if (const char* e = getenv("WG_STREAM_PPW")) stream_ppw_uniform = stream_ppw_mixed = std::max(1, atoi(e));
     if (const char* e = getenv("WG_STREAM_PPW_MIXED")) stream_ppw_mixed = std::max(1, atoi(e));
-    if (const char* e = getenv("WG_TRANSPORT_KERNEL")) use_tile_for_transport = strcmp(e, "tile") == 0;
+    if (const char* e = getenv("WG_TRANSPORT_KERNEL")) {
+      use_tile_for_transport = strcmp(e, "tile") == 0;
+      use_pipe = strcmp(e, "pipe") == 0;
+      use_lean = strcmp(e, "lean") == 0;
+    }
+    if (const char* e = getenv("WG_STREAM_VARIANT")) stream_variant = atoi(e) & 63;
     if (const char* e = getenv("WG_TILE_PASSES")) tile_passes = std::min(4u, std::max(1u, (uint32_t)atoi(e)));
     if (const char* e = getenv("WG_POLY_WAVES")) poly_waves = std::min(4u, std::max(1u, (uint32_t)atoi(e)));
     if (const char* e = getenv("WG_POLY_GMAX")) poly_gmax = std::min(64u, std::max(1u, (uint32_t)atoi(e)));
@@ -275,7 +283,18 @@ int launch_stream(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
   const uint32_t grid = (n + P.ppw - 1) / P.ppw;
   hipEvent_t ev;
   record_start(c, s, &ev);
-  hipLaunchKernelGGL((wgk::k_stream<MODE>), dim3(grid), dim3(64), 0, s, P);
+  if (tunables().use_lean) {
+    hipLaunchKernelGGL((wgk::k_lean<MODE>), dim3(grid), dim3(64), 0, s, P);
+  } else if (tunables().use_pipe) {
+    hipLaunchKernelGGL((wgk::k_pipe<MODE, 0>), dim3(grid), dim3(64), 0, s, P);
+  } else switch (tunables().stream_variant) {
+#define WG_CASE(V) \
+  case V: hipLaunchKernelGGL((wgk::k_stream<MODE, V>), dim3(grid), dim3(64), 0, s, P); break;
+    WG_CASE(0) WG_CASE(1) WG_CASE(2) WG_CASE(3) WG_CASE(4) WG_CASE(5) WG_CASE(6) WG_CASE(7)
+    WG_CASE(9) WG_CASE(11) WG_CASE(15) WG_CASE(17) WG_CASE(33) WG_CASE(49)
+    default: return fail(WG_EINVAL, "WG_STREAM_VARIANT %d not built", tunables().stream_variant);
+#undef WG_CASE
+  }
   hipError_t e = hipGetLastError();
   record_end(c, s, ev);
   if (e != hipSuccess) return fail(WG_EDEVICE, "k_stream launch: %s", hipGetErrorString(e));

@@ -46,6 +46,28 @@ __device__ __forceinline__ void chacha20_block(const uint32_t k[8], uint32_t ctr
   out[8] = x8 + k[4]; out[9] = x9 + k[5]; out[10] = x10 + k[6]; out[11] = x11 + k[7];
   out[12] = x12 + ctr; out[13] = x13 + n0; out[14] = x14 + n1; out[15] = x15 + n2;
 }
+// Same block, key read from LDS twice (before the rounds and again for the
+// feed-forward) so the 8 key words are not live across the 20 rounds; the
+// "memory" clobber keeps the compiler from merging the two reads.
+__device__ __forceinline__ void chacha20_block_lds(const uint4* key_lds, uint32_t ctr, uint32_t n0, uint32_t n1,
+                                                   uint32_t n2, uint32_t out[16]) {
+  uint4 ka = key_lds[0], kb = key_lds[1];
+  uint32_t x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
+  uint32_t x4 = ka.x, x5 = ka.y, x6 = ka.z, x7 = ka.w, x8 = kb.x, x9 = kb.y, x10 = kb.z, x11 = kb.w;
+  uint32_t x12 = ctr, x13 = n0, x14 = n1, x15 = n2;
+#pragma unroll 2
+  for (int r = 0; r < 10; ++r) {
+    WG_QR(x0, x4, x8, x12) WG_QR(x1, x5, x9, x13) WG_QR(x2, x6, x10, x14) WG_QR(x3, x7, x11, x15)
+    WG_QR(x0, x5, x10, x15) WG_QR(x1, x6, x11, x12) WG_QR(x2, x7, x8, x13) WG_QR(x3, x4, x9, x14)
+  }
+  asm volatile("" ::: "memory");
+  ka = key_lds[0];
+  kb = key_lds[1];
+  out[0] = x0 + 0x61707865u; out[1] = x1 + 0x3320646eu; out[2] = x2 + 0x79622d32u; out[3] = x3 + 0x6b206574u;
+  out[4] = x4 + ka.x; out[5] = x5 + ka.y; out[6] = x6 + ka.z; out[7] = x7 + ka.w;
+  out[8] = x8 + kb.x; out[9] = x9 + kb.y; out[10] = x10 + kb.z; out[11] = x11 + kb.w;
+  out[12] = x12 + ctr; out[13] = x13 + n0; out[14] = x14 + n1; out[15] = x15 + n2;
+}
 #undef WG_QR
 
 // ---- Poly1305, radix 2^26 -------------------------------------------------
@@ -92,6 +114,31 @@ __device__ __forceinline__ void poly_mul(uint32_t h[5], const uint32_t r[5], con
       (uint64_t)h3 * r[1] + (uint64_t)h4 * r[0];
   h[4] = (uint32_t)d & M26;
   uint32_t c = (uint32_t)(d >> 26);
+  h[0] += c * 5u;
+  c = h[0] >> 26; h[0] &= M26;
+  h[1] += c;
+}
+
+// Same product with the five limb sums as independent v_mad_u64_u32 chains
+// (ILP 5) and the carries applied afterwards with 64-bit adds: more instructions
+// than poly_mul, a much shorter dependent chain.
+__device__ __forceinline__ void poly_mul_ilp(uint32_t h[5], const uint32_t r[5], const uint32_t s[5]) {
+  uint64_t d0 = (uint64_t)h[0] * r[0] + (uint64_t)h[1] * s[4] + (uint64_t)h[2] * s[3] + (uint64_t)h[3] * s[2] +
+                (uint64_t)h[4] * s[1];
+  uint64_t d1 = (uint64_t)h[0] * r[1] + (uint64_t)h[1] * r[0] + (uint64_t)h[2] * s[4] + (uint64_t)h[3] * s[3] +
+                (uint64_t)h[4] * s[2];
+  uint64_t d2 = (uint64_t)h[0] * r[2] + (uint64_t)h[1] * r[1] + (uint64_t)h[2] * r[0] + (uint64_t)h[3] * s[4] +
+                (uint64_t)h[4] * s[3];
+  uint64_t d3 = (uint64_t)h[0] * r[3] + (uint64_t)h[1] * r[2] + (uint64_t)h[2] * r[1] + (uint64_t)h[3] * r[0] +
+                (uint64_t)h[4] * s[4];
+  uint64_t d4 = (uint64_t)h[0] * r[4] + (uint64_t)h[1] * r[3] + (uint64_t)h[2] * r[2] + (uint64_t)h[3] * r[1] +
+                (uint64_t)h[4] * r[0];
+  uint32_t c;
+  c = (uint32_t)(d0 >> 26); h[0] = (uint32_t)d0 & M26; d1 += c;
+  c = (uint32_t)(d1 >> 26); h[1] = (uint32_t)d1 & M26; d2 += c;
+  c = (uint32_t)(d2 >> 26); h[2] = (uint32_t)d2 & M26; d3 += c;
+  c = (uint32_t)(d3 >> 26); h[3] = (uint32_t)d3 & M26; d4 += c;
+  c = (uint32_t)(d4 >> 26); h[4] = (uint32_t)d4 & M26;
   h[0] += c * 5u;
   c = h[0] >> 26; h[0] &= M26;
   h[1] += c;

@@ -543,8 +543,10 @@ struct StreamParams {
   uint32_t* status;
 };
 
-template <int MODE>
-__global__ void __launch_bounds__(64) k_stream(StreamParams P) {
+// V (variant bits, for A/B builds; bits 4/5 are timing ablations that skip Poly1305 / the keystream): bit3 ILP form of the Poly1305 multiply, bit0 prefetch payload before the rounds,
+// bit1 re-read the key from LDS for the feed-forward, bit2 cap VGPRs for 8 waves/SIMD
+template <int MODE, int V>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((V & 4) ? 8 : 1))) k_stream(StreamParams P) {
   static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
   __shared__ uint4 img[8 * 8 * 4];  // [slot][lane][4 chunks]: the round's MAC input
   __shared__ uint4 skey[8 * 2];     // per-slot ChaCha key
@@ -597,12 +599,20 @@ __global__ void __launch_bounds__(64) k_stream(StreamParams P) {
     const uint32_t off = 64u * (b - 1u);
     const uint32_t nbytes = data ? min(64u, len - off) : 0u;
     uint32_t w[16];
-    if (data) load_block(P.in + in_off + off, nbytes, w);  // in flight during the rounds
+    if ((V & 1) && data) load_block(P.in + in_off + off, nbytes, w);  // in flight during the rounds
     if (act) {
-      const uint4 ka = skey[2 * s], kb = skey[2 * s + 1];
-      const uint32_t key[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
       uint32_t ks[16];
-      chacha20_block(key, b, ctr_lo, ctr_hi, 0u, ks);
+      if constexpr (V & 32) {  // ablation: no keystream
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ks[i] = ctr_lo + b * i;
+      } else if constexpr (V & 2) {
+        chacha20_block_lds(&skey[2 * s], b, ctr_lo, ctr_hi, 0u, ks);
+      } else {
+        const uint4 ka = skey[2 * s], kb = skey[2 * s + 1];
+        const uint32_t key[8] = {ka.x, ka.y, ka.z, ka.w, kb.x, kb.y, kb.z, kb.w};
+        chacha20_block(key, b, ctr_lo, ctr_hi, 0u, ks);
+      }
+      if (!(V & 1) && data) load_block(P.in + in_off + off, nbytes, w);
       if (!data) {
         sotk[2 * s] = make_uint4(ks[0], ks[1], ks[2], ks[3]);
         sotk[2 * s + 1] = make_uint4(ks[4], ks[5], ks[6], ks[7]);
@@ -623,7 +633,7 @@ __global__ void __launch_bounds__(64) k_stream(StreamParams P) {
     __syncthreads();
 
     // ---- Poly1305 ------------------------------------------------------------------
-    if (have && valid) {
+    if (!(V & 16) && have && valid) {
       if (round == 0) {  // r and its powers: lane j gets r^(j+1); R = r^8, W = r^(8-j)
         const uint4 o = sotk[2 * s];
         uint32_t x[5];
@@ -633,7 +643,7 @@ __global__ void __launch_bounds__(64) k_stream(StreamParams P) {
           uint32_t y[5], ys[5];
           shfl5(x, (int)(j >= st ? lane - st : lane), y);
           poly_scale5(y, ys);
-          if (j >= st) poly_mul(x, y, ys);
+          if (j >= st) { if constexpr (V & 8) poly_mul_ilp(x, y, ys); else poly_mul(x, y, ys); }
         }
         uint32_t R[5], W[5];
         shfl5(x, (int)(sbase + 7u), R);
@@ -661,7 +671,7 @@ __global__ void __launch_bounds__(64) k_stream(StreamParams P) {
       // first chunk c >= c_lo with (c + D) % 8 == j
       uint32_t c = c_lo + ((j - ((c_lo + D) & 7u)) & 7u);
       for (; c < c_end; c += 8u) {
-        poly_mul(acc, R, Rs);
+        if constexpr (V & 8) poly_mul_ilp(acc, R, Rs); else poly_mul(acc, R, Rs);
         uint32_t m0, m1, m2, m3;
         if (c < nc) {
           const uint32_t blk_lane = (c >> 2) + 1u - 8u * round;  // lane of the slot holding it
@@ -685,7 +695,7 @@ __global__ void __launch_bounds__(64) k_stream(StreamParams P) {
 #pragma unroll
         for (int i = 0; i < 5; ++i) W[i] = lpow[5 * lane + i];
         poly_scale5(W, Ws);
-        poly_mul(acc, W, Ws);
+        if constexpr (V & 8) poly_mul_ilp(acc, W, Ws); else poly_mul(acc, W, Ws);
 #pragma unroll
         for (uint32_t st = 1; st < 8u; st <<= 1) {
           uint32_t y[5];
@@ -740,6 +750,527 @@ __global__ void __launch_bounds__(64) k_stream(StreamParams P) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_pipe — k_stream's slot/round structure, software-pipelined: while a wave
+// computes round r out of one LDS stage buffer, round r+1's payload streams into
+// the other with coalesced global_load_lds_dwordx4 (1 KB per wave instruction, no
+// VGPRs), so every wave overlaps its own HBM traffic with its own ChaCha20 and
+// Poly1305 work instead of all waves alternating memory and compute in lockstep.
+// Slot s of wave w processes packets w*ppw + s, +8, +16, ... (static successor,
+// so the successor's descriptor and key are fetched a packet ahead).
+// Stage layout: [buffer][slot][32 x 16-byte chunks]; chunk c of round r of a
+// packet holds payload bytes 512r - 64 + 16c (round 0's chunks 0..3 are the key
+// block's place). Only whole 16-byte chunks of 16-byte aligned packets are
+// staged; a packet tail or an unaligned packet is read by its ChaCha lane.
+// The same buffer then holds the round's MAC input (ciphertext) for Poly1305.
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <int MODE, int V>
+__global__ void __launch_bounds__(64) k_pipe(StreamParams P) {
+  static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
+  __shared__ uint4 stage[2 * 256];  // 2 x 4 KB
+  __shared__ uint4 plan[8];         // per slot: {in_off lo, in_off hi, window start (signed), window end}
+  __shared__ uint4 skey[8 * 2];
+  __shared__ uint4 sotk[8 * 2];
+  __shared__ uint32_t spow[8 * 10];
+  __shared__ uint32_t lpow[64 * 5];
+  const uint32_t lane = threadIdx.x, s = lane >> 3, j = lane & 7u;
+  const uint32_t sbase = lane & ~7u;
+  const uint32_t w0 = blockIdx.x * P.ppw, w1 = min(P.n, w0 + P.ppw);
+
+  // current packet of the slot (identical in its 8 lanes)
+  uint32_t pkt = w0 + s;
+  bool have = pkt < w1;
+  uint64_t in_off = 0, out_off = 0;
+  uint32_t len = 0, ctr_lo = 0, ctr_hi = 0, nb = 0, nc = 0, D = 0, round = 0;
+  bool valid = false, staged = false;
+  uint32_t acc[5] = {0, 0, 0, 0, 0};
+  // successor descriptor (packet pkt + 8), fetched a packet ahead
+  uint4 sd_lo = make_uint4(0, 0, 0, 0), sd_hi = make_uint4(0, 0, 0, 0);
+  uint4 nk_a = make_uint4(0, 0, 0, 0), nk_b = make_uint4(0, 0, 0, 0);
+
+  auto decode = [&](uint4 lo, uint4 hi) {
+    in_off = (uint64_t)lo.x | ((uint64_t)lo.y << 32);
+    out_off = (uint64_t)lo.z | ((uint64_t)lo.w << 32);
+    ctr_lo = hi.x; ctr_hi = hi.y; len = hi.z;
+    valid = len <= P.max_len && hi.w < P.key_slots;
+    const uint64_t in_need = (uint64_t)len + (MODE == WG_MODE_OPEN ? 16u : 0u);
+    const uint64_t out_need = (uint64_t)len + (MODE == WG_MODE_SEAL ? 16u : 0u);
+    valid = valid && in_off <= P.in_size && in_need <= P.in_size - in_off;
+    valid = valid && out_off <= P.out_size && out_need <= P.out_size - out_off;
+    staged = valid && ((((uintptr_t)P.in + in_off) & 15u) == 0);
+    nb = ((len + 63u) >> 6) + 1u;
+    nc = (len + 15u) >> 4;
+    const uint32_t M = nc + 1u, K = (M + 7u) >> 3;
+    D = 8u * K - M;
+    round = 0;
+    acc[0] = acc[1] = acc[2] = acc[3] = acc[4] = 0;
+  };
+  auto write_plan = [&](bool any, uint32_t r) {
+    if (j == 0) {
+      const uint32_t full_end = staged && any ? (len & ~15u) : 0u;
+      plan[s] = make_uint4((uint32_t)in_off, (uint32_t)(in_off >> 32), 512u * r - 64u, full_end);
+    }
+  };
+  auto issue_stage = [&](uint32_t buf) {
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint32_t t = 2u * k + (lane >> 5), c = lane & 31u;
+      const uint4 pl = plan[t];
+      const int64_t o = (int64_t)(int32_t)pl.z + 16 * (int64_t)c;
+      if (o >= 0 && o + 16 <= (int64_t)pl.w) {
+        const uint64_t base = (uint64_t)pl.x | ((uint64_t)pl.y << 32);
+        __builtin_amdgcn_global_load_lds((const void*)(P.in + base + (uint64_t)o), (void*)&stage[buf * 256u + 64u * k],
+                                         16, 0, 0);
+      }
+    }
+  };
+
+  // ---- prologue: first packet of every slot, its key, its successor's descriptor
+  if (have) {
+    const uint4* dp = (const uint4*)(P.desc + pkt);
+    decode(dp[0], dp[1]);
+    if (j == 0 && valid) {
+      const uint4* kp = (const uint4*)(P.keys + 8u * ((const uint4*)(P.desc + pkt))[1].w);
+      skey[2 * s] = kp[0];
+      skey[2 * s + 1] = kp[1];
+    }
+    if (pkt + 8u < w1) {
+      const uint4* sp = (const uint4*)(P.desc + pkt + 8u);
+      sd_lo = sp[0];
+      sd_hi = sp[1];
+    }
+  }
+  write_plan(have, 0);
+  lds_fence();
+  issue_stage(0);
+  uint32_t buf = 0;
+
+  while (__any(have)) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this round's stage, keys, successor descriptors
+    const uint32_t nrounds = (nb + 7u) >> 3;
+    const bool last = have && (!valid || round + 1u >= nrounds);
+    const bool has_succ = pkt + 8u < w1;
+    // key of the successor: fetched now, published to LDS when it becomes current
+    if (have && last && has_succ && j == 0) {
+      const uint32_t ks_ = sd_hi.w < P.key_slots ? sd_hi.w : 0u;
+      const uint4* kp = (const uint4*)(P.keys + 8u * ks_);
+      nk_a = kp[0];
+      nk_b = kp[1];
+    }
+    // ---- plan and issue the next round's stage ---------------------------------
+    {
+      // decode the successor into temporaries only for planning
+      uint64_t t_in = in_off;
+      uint32_t t_len = len, r_next = round + 1u;
+      bool t_any = have && !last && valid;
+      bool t_staged = staged;
+      if (have && last && has_succ) {
+        t_in = (uint64_t)sd_lo.x | ((uint64_t)sd_lo.y << 32);
+        t_len = sd_hi.z;
+        r_next = 0;
+        t_any = t_len <= P.max_len && t_in <= P.in_size && (uint64_t)t_len <= P.in_size - t_in;
+        t_staged = ((((uintptr_t)P.in + t_in) & 15u) == 0);
+      }
+      if (j == 0) {
+        const uint32_t full_end = (t_any && t_staged) ? (t_len & ~15u) : 0u;
+        plan[s] = make_uint4((uint32_t)t_in, (uint32_t)(t_in >> 32), 512u * r_next - 64u, full_end);
+      }
+      lds_fence();
+      issue_stage(buf ^ 1u);
+    }
+
+    // ---- ChaCha20: block b of the slot's packet ------------------------------------
+    uint4* st = &stage[buf * 256u + 32u * s];  // this slot's 512 bytes
+    const uint32_t b = 8u * round + j;
+    const bool act = have && valid && b < nb;
+    const bool data = act && b > 0;
+    const uint32_t off = 64u * (b - 1u);
+    const uint32_t nbytes = data ? min(64u, len - off) : 0u;
+    if (act) {
+      uint32_t ks[16];
+      chacha20_block_lds(&skey[2 * s], b, ctr_lo, ctr_hi, 0u, ks);
+      if (!data) {
+        sotk[2 * s] = make_uint4(ks[0], ks[1], ks[2], ks[3]);
+        sotk[2 * s + 1] = make_uint4(ks[4], ks[5], ks[6], ks[7]);
+      } else {
+        uint32_t w[16];
+        if (staged) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int rem = (int)nbytes - 16 * i;
+            if (rem >= 16) {
+              const uint4 v = st[4u * j + i];
+              w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+            } else {
+              uint32_t t4[4];
+              load_chunk16(P.in + in_off + off + 16u * i, rem > 0 ? (uint32_t)rem : 0u, t4);
+              w[4 * i] = t4[0]; w[4 * i + 1] = t4[1]; w[4 * i + 2] = t4[2]; w[4 * i + 3] = t4[3];
+            }
+          }
+        } else {
+          load_block(P.in + in_off + off, nbytes, w);
+          if (nbytes < 64u) mask_block(nbytes, w);
+        }
+        if constexpr (MODE == WG_MODE_OPEN) {
+          if (!staged || nbytes < 64u) lds_store_block((uint8_t*)&st[4u * j], w);  // MAC input, zero padded
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] ^= ks[i];
+        store_block(P.out + out_off + off, nbytes, w);
+        if constexpr (MODE == WG_MODE_SEAL) {
+          if (nbytes < 64u) mask_block(nbytes, w);
+          lds_store_block((uint8_t*)&st[4u * j], w);  // MAC over the ciphertext just produced
+        }
+      }
+    }
+    lds_fence();
+
+    // ---- Poly1305 over this round's chunks -----------------------------------------------
+    if (have && valid) {
+      if (round == 0) {  // r and its powers: lane j gets r^(j+1); R = r^8, W = r^(8-j)
+        const uint4 o = sotk[2 * s];
+        uint32_t x[5];
+        poly_r_limbs(o.x, o.y, o.z, o.w, x);
+#pragma unroll
+        for (uint32_t stp = 1; stp < 8u; stp <<= 1) {
+          uint32_t y[5], ys[5];
+          shfl5(x, (int)(j >= stp ? lane - stp : lane), y);
+          poly_scale5(y, ys);
+          if (j >= stp) poly_mul(x, y, ys);
+        }
+        uint32_t R[5], W[5];
+        shfl5(x, (int)(sbase + 7u), R);
+        shfl5(x, (int)(sbase + 7u - j), W);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) lpow[5 * lane + i] = W[i];
+        if (j == 0) {
+#pragma unroll
+          for (int i = 0; i < 5; ++i) spow[10 * s + i] = R[i];
+#pragma unroll
+          for (int i = 1; i < 5; ++i) spow[10 * s + 5 + i] = R[i] * 5u;
+        }
+        lds_fence();
+      }
+      uint32_t R[5], Rs[5];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) R[i] = spow[10 * s + i];
+      Rs[0] = 0;
+#pragma unroll
+      for (int i = 1; i < 5; ++i) Rs[i] = spow[10 * s + 5 + i];
+      const uint32_t blo = max(8u * round, 1u);
+      const uint32_t c_lo = 4u * (blo - 1u);
+      const bool lastr = 8u * (round + 1u) >= nb;
+      const uint32_t c_end = lastr ? nc + 1u : min(nc, 4u * (8u * round + 7u));
+      uint32_t c = c_lo + ((j - ((c_lo + D) & 7u)) & 7u);
+      for (; c < c_end; c += 8u) {
+        poly_mul(acc, R, Rs);
+        uint32_t m0, m1, m2, m3;
+        if (c < nc) {
+          const uint4 v = st[c + 4u - 32u * round];
+          m0 = v.x; m1 = v.y; m2 = v.z; m3 = v.w;
+        } else {  // le64(0) || le64(len) (ChaCha20Poly1305.java:88-90)
+          m0 = 0; m1 = 0; m2 = len; m3 = 0;
+        }
+        uint32_t cl[5];
+        poly_block_limbs(m0, m1, m2, m3, 1u << 24, cl);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) acc[i] += cl[i];
+      }
+    }
+
+    // ---- finish packets whose last round this was ------------------------------------
+    if (last) {
+      if (valid) {
+        uint32_t W[5], Ws[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) W[i] = lpow[5 * lane + i];
+        poly_scale5(W, Ws);
+        poly_mul(acc, W, Ws);
+#pragma unroll
+        for (uint32_t stp = 1; stp < 8u; stp <<= 1) {
+          uint32_t y[5];
+          shfl5(acc, (int)(j + stp < 8u ? lane + stp : lane), y);
+          if (j + stp < 8u) {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) acc[i] += y[i];
+          }
+        }
+      }
+      uint32_t bad = valid ? 0u : 1u;
+      if (j == 0 && valid) {
+        const uint4 sv = sotk[2 * s + 1];
+        uint32_t tag[4];
+        poly_finish(acc, sv.x, sv.y, sv.z, sv.w, tag);
+        if constexpr (MODE == WG_MODE_SEAL) {
+          uint8_t* tp = P.out + out_off + len;
+          if ((((uintptr_t)tp) & 15u) == 0) {
+            *(uint4*)tp = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) store_u32_any(tp + 4 * i, tag[i]);
+          }
+        } else {
+          const uint8_t* tp = P.in + in_off + len;
+          uint32_t diff = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) diff |= load_u32_any(tp + 4 * i) ^ tag[i];
+          bad = diff ? 1u : 0u;
+        }
+      }
+      if constexpr (MODE == WG_MODE_OPEN) {
+        bad = __shfl(bad, (int)sbase, 64);
+        if (j == 0 && P.status) P.status[pkt] = bad ? WG_PKT_BADTAG : WG_PKT_OK;
+        if (bad && valid) {
+          uint8_t* o = P.out + out_off;
+          for (uint32_t i = j; i < len; i += 8u) o[i] = 0;
+        }
+      }
+      // advance to the successor
+      pkt += 8u;
+      have = pkt < w1;
+      if (have) {
+        decode(sd_lo, sd_hi);
+        if (j == 0 && valid) {
+          skey[2 * s] = nk_a;
+          skey[2 * s + 1] = nk_b;
+        }
+        if (pkt + 8u < w1) {
+          const uint4* sp = (const uint4*)(P.desc + pkt + 8u);
+          sd_lo = sp[0];
+          sd_hi = sp[1];
+        }
+      }
+    } else if (have) {
+      ++round;
+    }
+    lds_fence();
+    buf ^= 1u;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_lean — k_stream's slot/round algorithm with the register footprint cut to
+// <= 64 VGPRs (8 waves per SIMD): the slot's packet state, the per-lane Horner
+// accumulator and the Poly1305 powers live in LDS between uses, the key is read
+// from LDS on both sides of the rounds, and a block's payload is loaded after
+// its keystream (latency covered by the other waves). gfx950 issues dependent
+// add/xor streams at ~2.6 cycles only with ~8 waves per SIMD (tools/microbench4).
+//   slot record (16 words): in_off lo/hi, out_off lo/hi | ctr lo/hi, len, valid |
+//                           nb, nc, D, round | packet index (~0 = idle)
+template <int MODE>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) k_lean(StreamParams P) {
+  static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
+  __shared__ uint4 img[8 * 8 * 4];  // the round's MAC input, [slot][lane][4 chunks]
+  __shared__ uint4 srec[8 * 4];     // slot records
+  __shared__ uint4 skey[8 * 2];
+  __shared__ uint4 sotk[8 * 2];
+  __shared__ uint32_t spow[8 * 10];  // R = r^8 limbs, 5R limbs 1..4
+  __shared__ uint32_t lpow[64 * 5];  // W = r^(8-j) per lane
+  __shared__ uint32_t lacc[64 * 5];  // Horner accumulator per lane
+  const uint32_t lane = threadIdx.x, s = lane >> 3, j = lane & 7u;
+  const uint32_t sbase = lane & ~7u;
+  const uint32_t w0 = blockIdx.x * P.ppw, w1 = min(P.n, w0 + P.ppw);
+
+  // open packet `p` in slot `s` (called by the slot's lane j == 0)
+  auto open_packet = [&](uint32_t p) {
+    if (p >= w1) {
+      srec[4 * s + 3] = make_uint4(~0u, 0, 0, 0);
+      return;
+    }
+    const uint4* dp = (const uint4*)(P.desc + p);
+    const uint4 lo = dp[0], hi = dp[1];
+    const uint64_t in_off = (uint64_t)lo.x | ((uint64_t)lo.y << 32);
+    const uint64_t out_off = (uint64_t)lo.z | ((uint64_t)lo.w << 32);
+    const uint32_t len = hi.z;
+    bool valid = len <= P.max_len && hi.w < P.key_slots;
+    const uint64_t in_need = (uint64_t)len + (MODE == WG_MODE_OPEN ? 16u : 0u);
+    const uint64_t out_need = (uint64_t)len + (MODE == WG_MODE_SEAL ? 16u : 0u);
+    valid = valid && in_off <= P.in_size && in_need <= P.in_size - in_off;
+    valid = valid && out_off <= P.out_size && out_need <= P.out_size - out_off;
+    const uint32_t nb = ((len + 63u) >> 6) + 1u, nc = (len + 15u) >> 4;
+    const uint32_t M = nc + 1u, K = (M + 7u) >> 3;
+    srec[4 * s + 0] = lo;
+    srec[4 * s + 1] = make_uint4(hi.x, hi.y, len, valid ? 1u : 0u);
+    srec[4 * s + 2] = make_uint4(nb, nc, 8u * K - M, 0u);
+    srec[4 * s + 3] = make_uint4(p, 0, 0, 0);
+    if (valid) {
+      const uint4* kp = (const uint4*)(P.keys + 8u * hi.w);
+      skey[2 * s] = kp[0];
+      skey[2 * s + 1] = kp[1];
+    }
+  };
+
+  if (j == 0) open_packet(w0 + s);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) lacc[5 * lane + i] = 0;
+  uint32_t next = w0 + SLOT_LANES;  // wave-uniform
+  lds_fence();
+
+  while (true) {
+    const uint4 r3 = srec[4 * s + 3];
+    const bool have = r3.x != ~0u;
+    if (!__any(have)) break;
+    const uint4 r1 = srec[4 * s + 1];
+    const uint4 r2 = srec[4 * s + 2];
+    const bool valid = have && (r1.w & 1u);
+    const uint32_t len = r1.z, nb = r2.x, round = r2.w;
+
+    // ---- ChaCha20: block b of the slot's packet ------------------------------------
+    const uint32_t b = 8u * round + j;
+    if (valid && b < nb) {
+      uint32_t ks[16];
+      chacha20_block_lds(&skey[2 * s], b, r1.x, r1.y, 0u, ks);
+      if (b == 0) {
+        sotk[2 * s] = make_uint4(ks[0], ks[1], ks[2], ks[3]);
+        sotk[2 * s + 1] = make_uint4(ks[4], ks[5], ks[6], ks[7]);
+      } else {
+        const uint4 r0 = srec[4 * s];
+        const uint32_t off = 64u * (b - 1u);
+        const uint32_t n = min(64u, len - off);
+        uint32_t w[16];
+        load_block(P.in + ((uint64_t)r0.x | ((uint64_t)r0.y << 32)) + off, n, w);
+        if constexpr (MODE == WG_MODE_OPEN) {
+          if (n < 64u) mask_block(n, w);
+          lds_store_block((uint8_t*)&img[4 * lane], w);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] ^= ks[i];
+        store_block(P.out + ((uint64_t)r0.z | ((uint64_t)r0.w << 32)) + off, n, w);
+        if constexpr (MODE == WG_MODE_SEAL) {
+          if (n < 64u) mask_block(n, w);
+          lds_store_block((uint8_t*)&img[4 * lane], w);
+        }
+      }
+    }
+    lds_fence();
+
+    // ---- Poly1305 over this round's chunks ---------------------------------------------
+    if (valid) {
+      if (round == 0) {  // lane j gets r^(j+1) by a product scan; R = r^8, W = r^(8-j)
+        const uint4 o = sotk[2 * s];
+        uint32_t x[5];
+        poly_r_limbs(o.x, o.y, o.z, o.w, x);
+#pragma unroll
+        for (uint32_t st = 1; st < 8u; st <<= 1) {
+          uint32_t y[5], ys[5];
+          shfl5(x, (int)(j >= st ? lane - st : lane), y);
+          poly_scale5(y, ys);
+          if (j >= st) poly_mul(x, y, ys);
+        }
+        uint32_t t[5];
+        shfl5(x, (int)(sbase + 7u - j), t);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) lpow[5 * lane + i] = t[i];
+        shfl5(x, (int)(sbase + 7u), t);
+        if (j == 0) {
+#pragma unroll
+          for (int i = 0; i < 5; ++i) spow[10 * s + i] = t[i];
+#pragma unroll
+          for (int i = 1; i < 5; ++i) spow[10 * s + 5 + i] = t[i] * 5u;
+        }
+        lds_fence();
+      }
+      const uint32_t nc = r2.y, D = r2.z;
+      const uint32_t blo = max(8u * round, 1u);
+      const uint32_t c_lo = 4u * (blo - 1u);
+      const uint32_t c_end = (8u * (round + 1u) >= nb) ? nc + 1u : min(nc, 4u * (8u * round + 7u));
+      uint32_t c = c_lo + ((j - ((c_lo + D) & 7u)) & 7u);
+      if (c < c_end) {
+        uint32_t acc[5], R[5], Rs[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) acc[i] = lacc[5 * lane + i];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) R[i] = spow[10 * s + i];
+        Rs[0] = 0;
+#pragma unroll
+        for (int i = 1; i < 5; ++i) Rs[i] = spow[10 * s + 5 + i];
+        for (; c < c_end; c += 8u) {
+          poly_mul(acc, R, Rs);
+          uint32_t m0, m1, m2, m3;
+          if (c < nc) {
+            const uint4 v = img[4u * (sbase + (c >> 2) + 1u - 8u * round) + (c & 3u)];
+            m0 = v.x; m1 = v.y; m2 = v.z; m3 = v.w;
+          } else {  // le64(0) || le64(len) (ChaCha20Poly1305.java:88-90)
+            m0 = 0; m1 = 0; m2 = len; m3 = 0;
+          }
+          uint32_t cl[5];
+          poly_block_limbs(m0, m1, m2, m3, 1u << 24, cl);
+#pragma unroll
+          for (int i = 0; i < 5; ++i) acc[i] += cl[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) lacc[5 * lane + i] = acc[i];
+      }
+    }
+
+    // ---- finish packets whose last round this was ----------------------------------------
+    const bool done = have && (!valid || 8u * (round + 1u) >= nb);
+    if (done) {
+      uint32_t bad = valid ? 0u : 1u;
+      if (valid) {
+        uint32_t acc[5], W[5], Ws[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) acc[i] = lacc[5 * lane + i];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) W[i] = lpow[5 * lane + i];
+        poly_scale5(W, Ws);
+        poly_mul(acc, W, Ws);
+#pragma unroll
+        for (uint32_t st = 1; st < 8u; st <<= 1) {
+          uint32_t y[5];
+          shfl5(acc, (int)(j + st < 8u ? lane + st : lane), y);
+          if (j + st < 8u) {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) acc[i] += y[i];
+          }
+        }
+        if (j == 0) {
+          const uint4 sv = sotk[2 * s + 1];
+          const uint4 r0 = srec[4 * s];
+          uint32_t tag[4];
+          poly_finish(acc, sv.x, sv.y, sv.z, sv.w, tag);
+          if constexpr (MODE == WG_MODE_SEAL) {
+            uint8_t* tp = P.out + ((uint64_t)r0.z | ((uint64_t)r0.w << 32)) + len;
+            if ((((uintptr_t)tp) & 15u) == 0) {
+              *(uint4*)tp = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+            } else {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) store_u32_any(tp + 4 * i, tag[i]);
+            }
+          } else {
+            const uint8_t* tp = P.in + ((uint64_t)r0.x | ((uint64_t)r0.y << 32)) + len;
+            uint32_t diff = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) diff |= load_u32_any(tp + 4 * i) ^ tag[i];
+            bad = diff ? 1u : 0u;
+          }
+        }
+      }
+      if constexpr (MODE == WG_MODE_OPEN) {
+        bad = __shfl(bad, (int)sbase, 64);
+        if (j == 0 && P.status) P.status[r3.x] = bad ? WG_PKT_BADTAG : WG_PKT_OK;
+        if (bad && valid) {  // scrub the unauthenticated plaintext written this call
+          const uint4 r0 = srec[4 * s];
+          uint8_t* o = P.out + ((uint64_t)r0.z | ((uint64_t)r0.w << 32));
+          for (uint32_t i = j; i < len; i += 8u) o[i] = 0;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 5; ++i) lacc[5 * lane + i] = 0;
+    }
+    // hand the wave's next packets to the slots that finished (ballot rank)
+    const unsigned long long fin = __ballot(done && j == 0);
+    lds_fence();
+    if (j == 0 && have) {
+      if (done) open_packet(next + (uint32_t)__popcll(fin & ((1ull << sbase) - 1ull)));
+      else srec[4 * s + 2].w = round + 1u;
+    }
+    next += (uint32_t)__popcll(fin);
+    lds_fence();
+  }
+}
+
 // explicit instantiations used by wg_capi.hip
 template __global__ void k_tile<WG_MODE_SEAL, false>(TileParams);
 template __global__ void k_tile<WG_MODE_OPEN, false>(TileParams);
@@ -753,7 +1284,15 @@ template __global__ void k_plan_count<WG_MODE_SEAL, true>(const void*, uint32_t,
 template __global__ void k_plan_count<WG_MODE_OPEN, true>(const void*, uint32_t, uint32_t, uint32_t*);
 template __global__ void k_plan_count<WG_MODE_CIPHER, true>(const void*, uint32_t, uint32_t, uint32_t*);
 template __global__ void k_plan_count<WG_MODE_MAC, true>(const void*, uint32_t, uint32_t, uint32_t*);
-template __global__ void k_stream<WG_MODE_SEAL>(StreamParams);
-template __global__ void k_stream<WG_MODE_OPEN>(StreamParams);
+#define WG_STREAM_INST(V)                                                \
+  template __global__ void k_stream<WG_MODE_SEAL, V>(StreamParams); \
+  template __global__ void k_stream<WG_MODE_OPEN, V>(StreamParams);
+WG_STREAM_INST(0) WG_STREAM_INST(1) WG_STREAM_INST(2) WG_STREAM_INST(3)
+WG_STREAM_INST(4) WG_STREAM_INST(5) WG_STREAM_INST(6) WG_STREAM_INST(7)
+WG_STREAM_INST(9) WG_STREAM_INST(11) WG_STREAM_INST(15) WG_STREAM_INST(17) WG_STREAM_INST(33) WG_STREAM_INST(49)
+template __global__ void k_lean<WG_MODE_SEAL>(StreamParams);
+template __global__ void k_lean<WG_MODE_OPEN>(StreamParams);
+template __global__ void k_pipe<WG_MODE_SEAL, 0>(StreamParams);
+template __global__ void k_pipe<WG_MODE_OPEN, 0>(StreamParams);
 
 }  // namespace wgk

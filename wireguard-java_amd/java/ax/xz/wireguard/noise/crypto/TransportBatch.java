@@ -1,0 +1,114 @@
+package ax.xz.wireguard.noise.crypto;
+
+import java.lang.foreign.Arena;
+import java.lang.foreign.MemorySegment;
+
+import static java.lang.foreign.ValueLayout.*;
+
+/**
+ * The transport-data path on the MI355X: per-packet calls (what
+ * SymmetricKeypair.cipher/decipher make, SymmetricKeypair.java:63-83) and the
+ * batch calls a batching TransportManager makes (INTEGRATION.md §3).
+ *
+ * A batch is a table of 32-byte {@code wg_pkt} descriptors
+ * {in_off u64, out_off u64, counter u64, len u32, key_slot u32} over one input
+ * and one output buffer; seal writes ct || tag at out_off, open verifies then
+ * writes pt (status[i] = 1 and a zeroed pt for a forged packet).
+ */
+public final class TransportBatch {
+	private TransportBatch() {}
+
+	public static int installKeys(MemorySegment sendKey, MemorySegment receiveKey) {
+		return WgAead.installKeys(sendKey, receiveKey);
+	}
+
+	public static void releaseKeys(int sendSlot, int receiveSlot) {
+		WgAead.releaseKeys(sendSlot, receiveSlot);
+	}
+
+	/** dst (len + 16 bytes) = ChaCha20-Poly1305(key[slot], LE64(counter) || 0^4, src). */
+	public static void seal1(int slot, long counter, MemorySegment src, MemorySegment dst) {
+		try (var arena = Arena.ofConfined()) {
+			var in = native_(arena, src);
+			var out = dst.isNative() ? dst : arena.allocate(dst.byteSize(), 16);
+			WgAead.check((int) WgAead.SEAL1.invokeExact(WgAead.CTX, slot, counter, in, (int) src.byteSize(), out));
+			if (out != dst)
+				dst.copyFrom(out);
+		} catch (RuntimeException e) {
+			throw e;
+		} catch (Throwable e) {
+			throw new RuntimeException(e);
+		}
+	}
+
+	/** Verify-then-decrypt src = ct || tag into dst; false (dst untouched) on a bad tag. */
+	public static boolean open1(int slot, long counter, MemorySegment src, MemorySegment dst) {
+		try (var arena = Arena.ofConfined()) {
+			var in = native_(arena, src);
+			var out = arena.allocate(Math.max(1, dst.byteSize()), 16);
+			int rc = WgAead.check((int) WgAead.OPEN1.invokeExact(WgAead.CTX, slot, counter, in,
+				(int) (src.byteSize() - 16), out));
+			if (rc != 0)
+				return false;
+			dst.copyFrom(out.asSlice(0, dst.byteSize()));
+			return true;
+		} catch (RuntimeException e) {
+			throw e;
+		} catch (Throwable e) {
+			throw new RuntimeException(e);
+		}
+	}
+
+	/** Writes descriptor {@code i} of a wg_pkt table. */
+	public static void setPacket(MemorySegment table, int i, long inOff, long outOff, long counter, int len, int keySlot) {
+		long b = i * WgAead.PKT_DESC_SIZE;
+		table.set(JAVA_LONG, b, inOff);
+		table.set(JAVA_LONG, b + 8, outOff);
+		table.set(JAVA_LONG, b + 16, counter);
+		table.set(JAVA_INT, b + 24, len);
+		table.set(JAVA_INT, b + 28, keySlot);
+	}
+
+	/**
+	 * Seals {@code n} packets whose buffers live in device memory (pointers from a
+	 * device allocator); {@code stream} is the HIP stream to enqueue on (NULL: default).
+	 */
+	public static void sealDevice(MemorySegment table, int n, MemorySegment in, long inSize, MemorySegment out,
+	                              long outSize, int maxLen, boolean uniform, MemorySegment stream) {
+		try {
+			WgAead.check((int) WgAead.SEAL_BATCH.invokeExact(WgAead.CTX, table, n, in, inSize, out, outSize, maxLen,
+				uniform ? WgAead.WG_F_UNIFORM : 0, stream));
+		} catch (RuntimeException e) {
+			throw e;
+		} catch (Throwable e) {
+			throw new RuntimeException(e);
+		}
+	}
+
+	/** Opens {@code n} device-resident packets; status (device int32[n]) gets 0 / 1 per packet. */
+	public static void openDevice(MemorySegment table, int n, MemorySegment in, long inSize, MemorySegment out,
+	                              long outSize, MemorySegment status, int maxLen, boolean uniform, MemorySegment stream) {
+		try {
+			WgAead.check((int) WgAead.OPEN_BATCH.invokeExact(WgAead.CTX, table, n, in, inSize, out, outSize, status,
+				maxLen, uniform ? WgAead.WG_F_UNIFORM : 0, stream));
+		} catch (RuntimeException e) {
+			throw e;
+		} catch (Throwable e) {
+			throw new RuntimeException(e);
+		}
+	}
+
+	public static void sync(MemorySegment stream) {
+		try {
+			WgAead.check((int) WgAead.SYNC.invokeExact(WgAead.CTX, stream));
+		} catch (RuntimeException e) {
+			throw e;
+		} catch (Throwable e) {
+			throw new RuntimeException(e);
+		}
+	}
+
+	private static MemorySegment native_(Arena arena, MemorySegment s) {
+		return s.isNative() ? s : arena.allocate(Math.max(1, s.byteSize()), 16).copyFrom(s);
+	}
+}
