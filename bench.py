@@ -11,15 +11,21 @@ Workloads (--workload):
                 (BASELINE configs[1]; weak scaling: each rank owns its own sessions)
   c2            65536 packets per GPU, lengths uniform in [64, 9000], 256 session keys
   c3            8,388,608 x 1420 B in total, sharded by session over the ranks (strong)
+  c4            host-to-host (BASELINE configs[4]): 65536 x 1420 B from a host tun ring
+                to a host UDP ring (16-B headers, 1452-B stride) and back, through
+                wg_seal_host / wg_open_host; PCIe-inclusive, reported in DESIGN.md,
+                never the headline value. --host-mem pinned (zero-copy or, with
+                WG_HOST_PATH=copy, the copy pipeline) or pageable (copy pipeline)
 
 Multi-GPU: one process per GPU (torchrun); packets are independent, so each rank
 works on its own shard — no collective on the data path. The only collectives
 are the timing barrier and the max-over-ranks reduction.
 
 The JSON line also carries:
-  roofline      the seal kernel (k_stream<SEAL>) against the 8 TB/s HBM peak, with
-                algorithmic bytes = n * (2L + 16) per launch and the launch duration
-                from HIP events on the launch stream; `traffic` from the committed
+  roofline      the transport kernel (k_stream, seal and open launches) against the
+                8 TB/s HBM peak: achieved = sum(4L + 32) per step / GPU time per step
+                (SURVEY.md §8d), GPU time from HIP events on the launch stream around
+                the timed region; `traffic` = HBM bytes per launch from the committed
                 rocprofv3 PMC summary (profiles/pmc_*.json) when present
   cpu_baseline  the CPU restatement (oracle/liboracle.so, bit-exact to the
                 reference) timed on this host's cores, rank 0, N = 1 only
@@ -118,15 +124,74 @@ def cpu_baseline(lengths, slots, counters, keys, budget_s: float = 1.5):
 
 
 def pmc_traffic():
-    """Per-launch HBM bytes of the seal kernel from the newest committed PMC summary."""
+    """Per-launch HBM bytes of k_stream (mean of the seal and open launches) from the
+    newest committed PMC summary (profiles/pmc_*.json, written by tools/pmc_to_json.py)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
     if not files:
         return None
     try:
         d = json.load(open(files[-1]))
-        return d.get("seal_hbm_bytes_per_launch")
+        v = [d[k] for k in ("seal_hbm_bytes_per_launch", "open_hbm_bytes_per_launch") if k in d]
+        return round(sum(v) / len(v)) if v else None
     except Exception:
         return None
+
+
+def host_bench(args):
+    """configs[4]: tun ring -> seal -> UDP ring -> open -> tun ring, buffers in host memory."""
+    import torch
+    wg = importlib.import_module("wireguard-java_amd")
+    n, L, tun_stride = 65536, 1420, 1440
+    wire = 16 + L + 16
+    eng = wg.Engine(0, key_slots=1)
+    eng.set_keys(0, splitmix_np(0xC0FFEE, 32).tobytes())
+    sd = wg.pack_desc(np.arange(n, dtype=np.uint64) * tun_stride, np.arange(n, dtype=np.uint64) * wire + 16,
+                      np.arange(n, dtype=np.uint64), L, 0)
+    od = sd.copy()
+    od["in_off"], od["out_off"] = sd["out_off"], sd["in_off"]
+    if args.host_mem == "pinned":
+        tun, ring, back = eng.host_alloc(n * tun_stride), eng.host_alloc(n * wire), eng.host_alloc(n * tun_stride)
+    else:
+        tun, ring, back = (np.empty(n * tun_stride, np.uint8), np.empty(n * wire, np.uint8),
+                           np.empty(n * tun_stride, np.uint8))
+    tun[:] = splitmix_np(0x5EED2026, n * tun_stride)
+    ring[:] = 0
+    back[:] = 0
+
+    def step():
+        eng.seal_host(sd, tun, ring, L, uniform=True)
+        st = eng.open_host(od, ring, back, L, uniform=True)
+        return st
+
+    for _ in range(args.warmup):
+        step()
+    seal_t = open_t = 0.0
+    for _ in range(args.steps):
+        t0 = time.perf_counter()
+        eng.seal_host(sd, tun, ring, L, uniform=True)
+        t1 = time.perf_counter()
+        st = eng.open_host(od, ring, back, L, uniform=True)
+        t2 = time.perf_counter()
+        seal_t += t1 - t0
+        open_t += t2 - t1
+    ok = not st.any() and np.array_equal(back.reshape(n, tun_stride)[:, :L], tun.reshape(n, tun_stride)[:, :L])
+    payload = 2.0 * n * L * args.steps
+    mode = os.environ.get("WG_HOST_PATH", "auto")
+    path = "zero-copy" if args.host_mem == "pinned" and mode != "copy" else "copy pipeline"
+    print(json.dumps({
+        "metric": "host-to-host AEAD GiB/s (PCIe-inclusive), 64K x 1420B seal+open, 1 MI355X",
+        "value": round(payload / (seal_t + open_t) / GIB, 2), "unit": "GiB/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round((seal_t + open_t) * 1e3 / args.steps, 3), "higher_is_better": True,
+        "seal_ms": round(seal_t * 1e3 / args.steps, 3), "open_ms": round(open_t * 1e3 / args.steps, 3),
+        "host_mem": args.host_mem, "path": path, "verified": bool(ok),
+        "config": {"workload": "C4: tun ring (1440-B slots) -> UDP ring (16-B header + ct||tag, 1452-B stride) "
+                               "-> tun ring, 65536 x 1420B, host buffers"}}), flush=True)
+    if args.host_mem == "pinned":
+        for a in (tun, ring, back):
+            eng.host_free(a)
+    eng.close()
+    del torch
 
 
 def main():
@@ -134,9 +199,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c1", choices=["c1", "c2", "c3"])
+    ap.add_argument("--workload", default="c1", choices=["c1", "c2", "c3", "c4"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-mem", default="pinned", choices=["pinned", "pageable"])
     args = ap.parse_args()
+    if args.workload == "c4":
+        return host_bench(args)
 
     import torch
     import torch.distributed as dist
@@ -171,50 +239,63 @@ def main():
     status = torch.zeros(n, dtype=torch.int32, device=dev)
     max_len = int(lengths.max())
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record()
+    def step():
         eng.seal(d_desc, pt, ct, max_len, uniform=uniform)
-        if ev is not None:
-            ev[1].record()
         eng.open(d_desc, ct, back, status, max_len, uniform=uniform)
-        if ev is not None:
-            ev[2].record()
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
 
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    # HIP events on the stream the kernels are launched on (torch's current stream,
+    # which Engine passes to wg_seal_batch / wg_open_batch), around the whole region
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(events[k])
+    ev0.record()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
-    seal_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
-    open_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
+    gpu_step_ms = ev0.elapsed_time(ev1) / args.steps  # = t_seal + t_open (back-to-back launches)
+
+    # per-kernel split (not in the timed region): seal-only and open-only launch trains
+    def train(fn, k=10):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(k):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / k
+    seal_ms = train(lambda: eng.seal(d_desc, pt, ct, max_len, uniform=uniform))
+    open_ms = train(lambda: eng.open(d_desc, ct, back, status, max_len, uniform=uniform))
 
     # correctness guard on the device: open(seal(x)) == x, every tag verified
     ok_status = int(status.abs().sum().item()) == 0
-    mask = torch.zeros(total, dtype=torch.bool, device=dev)
-    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
-    d_len = torch.from_numpy(lengths).to(dev)
-    idx = torch.arange(total, device=dev)
-    pkt = torch.searchsorted(d_off, idx, right=True) - 1
-    mask = (idx - d_off[pkt]) < d_len[pkt]
-    ok_data = bool(torch.equal(back[mask], pt[mask]))
+    if uniform:  # equal strides: compare the [n, L] payload views directly
+        s0, L0 = int(S[0]), int(lengths[0])
+        ok_data = bool(torch.equal(back.view(n, s0)[:, :L0], pt.view(n, s0)[:, :L0]))
+    else:
+        d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+        d_len = torch.from_numpy(lengths).to(dev)
+        idx = torch.arange(total, device=dev)
+        pkt = torch.searchsorted(d_off, idx, right=True) - 1
+        mask = (idx - d_off[pkt]) < d_len[pkt]
+        ok_data = bool(torch.equal(back[mask], pt[mask]))
+        del idx, pkt, mask
 
     payload = 2.0 * float(lengths.sum())  # sealed + opened bytes per step on this rank
     if world > 1:
-        t = torch.tensor([elapsed, seal_ms, open_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, seal_ms, open_ms, gpu_step_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, seal_ms, open_ms = t.tolist()
+        elapsed, seal_ms, open_ms, gpu_step_ms = t.tolist()
         p = torch.tensor([payload], dtype=torch.float64, device=dev)
         dist.all_reduce(p)
         payload_all = p.item()
@@ -226,8 +307,9 @@ def main():
         all_ok = ok_status and ok_data
 
     value = payload_all * args.steps / elapsed / GIB
-    seal_alg = float((2 * lengths + 16).sum())  # read L + write L+16 per packet
-    achieved = seal_alg / (seal_ms * 1e-3) / 1e9
+    # seal reads L, writes L+16; open reads L+16, writes L -> 4L+32 per packet
+    step_alg = float((4 * lengths + 32).sum())
+    achieved = step_alg / (gpu_step_ms * 1e-3) / 1e9
     traffic = pmc_traffic() if args.workload == "c1" else None
 
     if rank == 0:
@@ -246,10 +328,11 @@ def main():
             "data": "synthetic (random payload in HBM, splitmix64 keys, sequential counters)",
             "config": {"workload": wdesc, "packets_per_gpu": n, "payload_bytes": int(lengths.mean()),
                        "sessions_per_gpu": nkeys, "parallelism": f"dp{world} sharded by session, no collective"},
-            "roofline": {"bound": "hbm", "kernel": "k_stream<SEAL>", "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": "k_stream<SEAL|OPEN>", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "seal_ms": round(seal_ms, 4), "open_ms": round(open_ms, 4),
-                         "alg_bytes_per_launch": int(seal_alg)},
+                         "traffic": traffic, "alg_bytes_per_launch": int(step_alg / 2),
+                         "kernel_ms": round(gpu_step_ms / 2, 5), "seal_ms": round(seal_ms, 5),
+                         "open_ms": round(open_ms, 5)},
             "verified": all_ok,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -146,14 +146,27 @@ int wg_aead_batch(wg_ctx* ctx, int mode, const wg_aead_desc* desc_dev, uint32_t 
  *   cipher(src, dst): wg_seal1(ctx, send_slot, counter, src, L, dst) with dst of L+16 bytes
  *   decipher(counter, src, dst): wg_open1(ctx, recv_slot, counter, src, L, dst) with src of L+16 bytes
  *   returns WG_OK, or 1 for a bad tag (dst untouched, as NOISE/crypto/ChaCha20Poly1305.java:51-55).
- * wg_seal_host / wg_open_host: a batch in host memory (tun ring in, UDP ring out),
- *   pipelined H2D -> kernel -> D2H in chunks over two streams. */
+ * wg_seal_host / wg_open_host: a batch in host memory (tun ring in, UDP ring out).
+ *   If `in` and `out` are pinned, device-mapped host memory (wg_host_alloc /
+ *   wg_host_register) the kernel reads and writes them directly over PCIe
+ *   (zero-copy); otherwise the batch moves through device mirrors in chunks with
+ *   H2D, kernel and D2H overlapped on three streams. Only packet bytes are written
+ *   to `out_host` (bytes between packets — wire headers, ring slack — are kept).
+ *   On a bad tag the plaintext range is zero-filled and status[i] = WG_PKT_BADTAG. */
 int wg_seal1(wg_ctx* ctx, uint32_t key_slot, uint64_t counter, const uint8_t* pt, uint32_t len, uint8_t* out);
 int wg_open1(wg_ctx* ctx, uint32_t key_slot, uint64_t counter, const uint8_t* in, uint32_t len, uint8_t* pt);
 int wg_seal_host(wg_ctx* ctx, const wg_pkt* desc_host, uint32_t n, const uint8_t* in_host, uint64_t in_size,
                  uint8_t* out_host, uint64_t out_size, uint32_t max_len, uint32_t flags);
 int wg_open_host(wg_ctx* ctx, const wg_pkt* desc_host, uint32_t n, const uint8_t* in_host, uint64_t in_size,
                  uint8_t* out_host, uint64_t out_size, uint32_t* status_host, uint32_t max_len, uint32_t flags);
+/* Pinned host rings for the host path (the reference's packet buffers come from
+ * a native pool, Pool.java:96; pinning them makes wg_seal_host/wg_open_host zero-copy).
+ * wg_host_alloc: page-locked, device-mapped, portable across devices.
+ * wg_host_register: pin existing memory (e.g. a Java Arena segment) in place. */
+int wg_host_alloc(wg_ctx* ctx, uint64_t bytes, void** out);
+int wg_host_free(wg_ctx* ctx, void* p);
+int wg_host_register(wg_ctx* ctx, void* p, uint64_t bytes);
+int wg_host_unregister(wg_ctx* ctx, void* p);
 /* General AEAD / primitives on host buffers with a per-call key list
  * (desc[i].key_slot indexes keys_host[nkeys][32]); the device copy of the keys
  * is zeroed before returning. */

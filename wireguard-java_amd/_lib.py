@@ -76,6 +76,10 @@ SIGNATURES = [
     ("wg_open1", _I, [_VP, _U32, _U64, _VP, _U32, _VP]),
     ("wg_seal_host", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _U32, _U32]),
     ("wg_open_host", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _VP, _U32, _U32]),
+    ("wg_host_alloc", _I, [_VP, _U64, ctypes.POINTER(_VP)]),
+    ("wg_host_free", _I, [_VP, _VP]),
+    ("wg_host_register", _I, [_VP, _VP, _U64]),
+    ("wg_host_unregister", _I, [_VP, _VP]),
     ("wg_aead_host", _I, [_VP, _I, _VP, _U32, _VP, _U32, _VP, _U64, _VP, _U64, _VP, _U64, _VP]),
     ("wg_timing_enable", _I, [_VP, _I]),
     ("wg_timing_read", _I, [_VP, ctypes.POINTER(_D), ctypes.POINTER(_U64)]),

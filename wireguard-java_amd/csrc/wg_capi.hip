@@ -69,7 +69,9 @@ struct DevBuf {
 struct wg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipStream_t copy_stream = nullptr;
+  hipStream_t copy_stream = nullptr;      // host path: H2D
+  hipStream_t copy_out_stream = nullptr;  // host path: D2H
+  hipEvent_t ev_desc = nullptr, ev_in = nullptr, ev_kernel = nullptr;
   uint32_t key_slots = 0;
   uint32_t* keys = nullptr;  // device key table
   // non-uniform plan workspace
@@ -115,7 +117,9 @@ struct Tunables {
   int stream_variant = 1;                                   // k_stream<MODE, V> variant bits
   int use_pipe = 0;                                         // k_pipe (software-pipelined) for transport
   int use_lean = 0;                                         // k_lean (state in LDS) for transport
+  uint32_t stream_lds_pad = 0;                              // dynamic LDS per wave: caps occupancy
   Tunables() {
+    if (const char* e = getenv("WG_STREAM_LDS_PAD")) stream_lds_pad = (uint32_t)std::min(65536, std::max(0, atoi(e)));
     if (const char* e = getenv("WG_STREAM_PPW")) stream_ppw_uniform = stream_ppw_mixed = std::max(1, atoi(e));
     if (const char* e = getenv("WG_STREAM_PPW_MIXED")) stream_ppw_mixed = std::max(1, atoi(e));
     if (const char* e = getenv("WG_TRANSPORT_KERNEL")) {
@@ -281,6 +285,7 @@ int launch_stream(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
   P.keys = c->keys;
   P.status = status;
   const uint32_t grid = (n + P.ppw - 1) / P.ppw;
+  const uint32_t pad = tunables().stream_lds_pad;
   hipEvent_t ev;
   record_start(c, s, &ev);
   if (tunables().use_lean) {
@@ -289,7 +294,7 @@ int launch_stream(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
     hipLaunchKernelGGL((wgk::k_pipe<MODE, 0>), dim3(grid), dim3(64), 0, s, P);
   } else switch (tunables().stream_variant) {
 #define WG_CASE(V) \
-  case V: hipLaunchKernelGGL((wgk::k_stream<MODE, V>), dim3(grid), dim3(64), 0, s, P); break;
+  case V: hipLaunchKernelGGL((wgk::k_stream<MODE, V>), dim3(grid), dim3(64), pad, s, P); break;
     WG_CASE(0) WG_CASE(1) WG_CASE(2) WG_CASE(3) WG_CASE(4) WG_CASE(5) WG_CASE(6) WG_CASE(7)
     WG_CASE(9) WG_CASE(11) WG_CASE(15) WG_CASE(17) WG_CASE(33) WG_CASE(49)
     default: return fail(WG_EINVAL, "WG_STREAM_VARIANT %d not built", tunables().stream_variant);
@@ -339,6 +344,10 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   c->key_slots = key_slots;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->copy_out_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_desc, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_kernel, hipEventDisableTiming) != hipSuccess ||
       hipMalloc(&c->keys, (size_t)key_slots * 32) != hipSuccess ||
       hipMemset(c->keys, 0, (size_t)key_slots * 32) != hipSuccess) {
     wg_ctx_destroy(c);
@@ -365,6 +374,9 @@ int wg_ctx_destroy(wg_ctx* c) {
     b->release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+  if (c->copy_out_stream) (void)hipStreamDestroy(c->copy_out_stream);
+  for (hipEvent_t e : {c->ev_desc, c->ev_in, c->ev_kernel})
+    if (e) (void)hipEventDestroy(e);
   delete c;
   return WG_OK;
 }
@@ -440,35 +452,193 @@ int wg_aead_batch(wg_ctx* c, int mode, const wg_aead_desc* desc, uint32_t n, con
 }
 
 // ---- host-pointer API --------------------------------------------------------
+//
+// The transport path starts and ends in host memory (tun device in, UDP socket out).
+// Two strategies, chosen per call (WG_HOST_PATH=auto|copy|zerocopy overrides):
+//  * zero-copy: when `in` and `out` are pinned, device-mapped host memory
+//    (wg_host_alloc, wg_host_register, or a pinned torch tensor), the kernel reads
+//    the plaintext/ciphertext over PCIe and writes the result straight into the
+//    caller's ring — every byte crosses the link once, in both directions at once;
+//  * copy pipeline: otherwise the batch is cut into chunks of consecutive packets
+//    and H2D(chunk k+1) / kernel(chunk k) / D2H(chunk k-1) overlap on three streams.
+//    Chunks whose packets sit at a uniform stride move only their payload bytes
+//    (hipMemcpy2DAsync rows), so bytes between packets (wire headers, ring slack)
+//    are left untouched; irregular layouts move whole ranges and stage `out` first.
+namespace {
+
+// device alias of pinned, mapped host memory, or nullptr for pageable memory
+uint8_t* mapped_alias(const void* p) {
+  if (!p) return nullptr;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+  uint8_t* d = (uint8_t*)a.devicePointer;
+  if (a.hostPointer) d += (const uint8_t*)p - (const uint8_t*)a.hostPointer;
+  return d;
+}
+
+int host_path_mode() {  // 0 auto, 1 copy, 2 zerocopy
+  static int m = [] {
+    const char* e = getenv("WG_HOST_PATH");
+    if (!e) return 0;
+    if (!strcmp(e, "copy")) return 1;
+    if (!strcmp(e, "zerocopy")) return 2;
+    return 0;
+  }();
+  return m;
+}
+
+uint64_t host_chunk_bytes() {
+  static uint64_t b = [] {
+    const char* e = getenv("WG_HOST_CHUNK");
+    uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
+    return v ? v : (uint64_t)8 << 20;
+  }();
+  return b;
+}
+
+// one chunk's footprint in a buffer: [lo, hi), and whether its packets sit at a
+// uniform stride with equal lengths (then only `width` bytes per row are copied)
+struct Span {
+  uint64_t lo = ~0ull, hi = 0, stride = 0, width = 0;
+  bool rows = false;
+};
+
+Span chunk_span(const wg_pkt* d, uint32_t a, uint32_t b, bool in_side, uint32_t extra) {
+  Span sp;
+  const uint64_t first = in_side ? d[a].in_off : d[a].out_off;
+  const uint64_t second = (b - a > 1) ? (in_side ? d[a + 1].in_off : d[a + 1].out_off) : first;
+  const uint64_t stride = second > first ? second - first : 0;  // descending order: no row copy
+  bool uni = b - a == 1 || stride > 0;
+  for (uint32_t i = a; i < b; ++i) {
+    const uint64_t o = in_side ? d[i].in_off : d[i].out_off;
+    const uint64_t e = o + d[i].len + extra;
+    sp.lo = std::min(sp.lo, o);
+    sp.hi = std::max(sp.hi, e);
+    uni = uni && d[i].len == d[a].len && o == first + (uint64_t)(i - a) * stride;
+  }
+  sp.width = (uint64_t)d[a].len + extra;
+  sp.stride = stride;
+  sp.rows = uni && (b - a == 1 || stride >= sp.width);
+  return sp;
+}
+
+int copy_span(uint8_t* dst, const uint8_t* src, const Span& sp, uint32_t rows, hipMemcpyKind k, hipStream_t s) {
+  if (sp.hi <= sp.lo) return WG_OK;
+  if (sp.rows && rows > 1 && sp.stride != sp.width) {
+    HIPTRY(hipMemcpy2DAsync(dst + sp.lo, sp.stride, src + sp.lo, sp.stride, sp.width, rows, k, s));
+  } else {
+    HIPTRY(hipMemcpyAsync(dst + sp.lo, src + sp.lo, sp.hi - sp.lo, k, s));
+  }
+  return WG_OK;
+}
+
+}  // namespace
 
 static int host_transport(wg_ctx* c, bool open, const wg_pkt* desc, uint32_t n, const uint8_t* in, uint64_t in_size,
                           uint8_t* out, uint64_t out_size, uint32_t* status, uint32_t max_len, uint32_t flags) {
   if (!c || (n && (!desc || !in || !out))) return fail(WG_EINVAL, "NULL argument");
   if (open && n && !status) return fail(WG_EINVAL, "open needs a status array");
   if (!n) return WG_OK;
+  if (max_len > WG_MAX_PACKET) return fail(WG_E2BIG, "max_len %u > WG_MAX_PACKET", max_len);
   DeviceGuard g(c->device);
   std::lock_guard<std::mutex> lk(c->mu);
   int rc;
-  if ((rc = c->h_desc.ensure(sizeof(wg_pkt) * (size_t)n)) || (rc = c->h_in.ensure(in_size)) ||
-      (rc = c->h_out.ensure(out_size)) || (rc = c->h_status.ensure(sizeof(uint32_t) * (size_t)n)))
+  if ((rc = c->h_desc.ensure(sizeof(wg_pkt) * (size_t)n)) || (rc = c->h_status.ensure(sizeof(uint32_t) * (size_t)n)))
     return rc;
-  hipStream_t s = c->stream;
+  hipStream_t s = c->stream, sin = c->copy_stream, sout = c->copy_out_stream;
   HIPTRY(hipMemcpyAsync(c->h_desc.p, desc, sizeof(wg_pkt) * (size_t)n, hipMemcpyHostToDevice, s));
-  HIPTRY(hipMemcpyAsync(c->h_in.p, in, in_size, hipMemcpyHostToDevice, s));
-  if (open) {
-    // the caller's plaintext buffer must stay untouched on failure: stage it
-    HIPTRY(hipMemcpyAsync(c->h_out.p, out, out_size, hipMemcpyHostToDevice, s));
-    rc = launch_transport<WG_MODE_OPEN>(c, (const wg_pkt*)c->h_desc.p, n, (const uint8_t*)c->h_in.p, in_size,
-                                        (uint8_t*)c->h_out.p, out_size, (uint32_t*)c->h_status.p, max_len, flags, s);
-  } else {
-    HIPTRY(hipMemcpyAsync(c->h_out.p, out, out_size, hipMemcpyHostToDevice, s));
-    rc = launch_transport<WG_MODE_SEAL>(c, (const wg_pkt*)c->h_desc.p, n, (const uint8_t*)c->h_in.p, in_size,
-                                        (uint8_t*)c->h_out.p, out_size, nullptr, max_len, flags, s);
+  const wg_pkt* ddesc = (const wg_pkt*)c->h_desc.p;
+  uint32_t* dstatus = (uint32_t*)c->h_status.p;
+
+  const int mode = host_path_mode();
+  uint8_t* zin = mode == 1 ? nullptr : mapped_alias(in);
+  uint8_t* zout = mode == 1 ? nullptr : mapped_alias(out);
+  if (mode == 2 && (!zin || !zout)) return fail(WG_EINVAL, "WG_HOST_PATH=zerocopy needs pinned host buffers");
+  if (zin && zout) {
+    rc = open ? launch_transport<WG_MODE_OPEN>(c, ddesc, n, zin, in_size, zout, out_size, dstatus, max_len, flags, s)
+              : launch_transport<WG_MODE_SEAL>(c, ddesc, n, zin, in_size, zout, out_size, nullptr, max_len, flags, s);
+    if (rc) return rc;
+    if (open) HIPTRY(hipMemcpyAsync(status, dstatus, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, s));
+    HIPTRY(hipStreamSynchronize(s));
+    return WG_OK;
   }
-  if (rc) return rc;
-  if (open) HIPTRY(hipMemcpyAsync(status, c->h_status.p, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, s));
-  HIPTRY(hipMemcpyAsync(out, c->h_out.p, out_size, hipMemcpyDeviceToHost, s));
+
+  // copy pipeline over full-size device mirrors of the two buffers
+  if ((rc = c->h_in.ensure(in_size)) || (rc = c->h_out.ensure(out_size))) return rc;
+  uint8_t* din = (uint8_t*)c->h_in.p;
+  uint8_t* dout = (uint8_t*)c->h_out.p;
+  const uint32_t in_extra = open ? 16u : 0u, out_extra = open ? 0u : 16u;
+  uint64_t per = host_chunk_bytes() / ((uint64_t)max_len + 32u);
+  uint32_t chunk = (uint32_t)std::min<uint64_t>(n, std::max<uint64_t>(per, 64));
+  // the chunks must occupy increasing, disjoint ranges of both buffers, or one chunk's
+  // staged copy of `out` could overwrite another's results: otherwise use one chunk
+  {
+    uint64_t prev_in = 0, prev_out = 0;
+    for (uint32_t a = 0; a < n; a += chunk) {
+      const uint32_t b = std::min(n, a + chunk);
+      const Span si = chunk_span(desc, a, b, true, in_extra), so = chunk_span(desc, a, b, false, out_extra);
+      if (a && (si.lo < prev_in || so.lo < prev_out)) { chunk = n; break; }
+      prev_in = si.hi;
+      prev_out = so.hi;
+    }
+  }
+  HIPTRY(hipEventRecord(c->ev_desc, s));
+  HIPTRY(hipStreamWaitEvent(sin, c->ev_desc, 0));
+  for (uint32_t a = 0; a < n; a += chunk) {
+    const uint32_t b = std::min(n, a + chunk), rows = b - a;
+    const Span si = chunk_span(desc, a, b, true, in_extra), so = chunk_span(desc, a, b, false, out_extra);
+    if ((rc = copy_span(din, in, si, rows, hipMemcpyHostToDevice, sin))) return rc;
+    // a range (not row) copy back would overwrite the bytes between packets: stage them
+    if (!(so.rows && rows > 1 && so.stride != so.width) && (so.hi - so.lo) != (uint64_t)rows * so.width)
+      HIPTRY(hipMemcpyAsync(dout + so.lo, out + so.lo, so.hi - so.lo, hipMemcpyHostToDevice, sin));
+    HIPTRY(hipEventRecord(c->ev_in, sin));
+    HIPTRY(hipStreamWaitEvent(s, c->ev_in, 0));
+    rc = open ? launch_transport<WG_MODE_OPEN>(c, ddesc + a, rows, din, in_size, dout, out_size, dstatus + a, max_len,
+                                               flags, s)
+              : launch_transport<WG_MODE_SEAL>(c, ddesc + a, rows, din, in_size, dout, out_size, nullptr, max_len,
+                                               flags, s);
+    if (rc) return rc;
+    HIPTRY(hipEventRecord(c->ev_kernel, s));
+    HIPTRY(hipStreamWaitEvent(sout, c->ev_kernel, 0));
+    if ((rc = copy_span(out, dout, so, rows, hipMemcpyDeviceToHost, sout))) return rc;
+  }
+  if (open) HIPTRY(hipMemcpyAsync(status, dstatus, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, sout));
+  HIPTRY(hipStreamSynchronize(sout));
   HIPTRY(hipStreamSynchronize(s));
+  return WG_OK;
+}
+
+int wg_host_alloc(wg_ctx* c, uint64_t bytes, void** out) {
+  if (!c || !out) return fail(WG_EINVAL, "NULL argument");
+  *out = nullptr;
+  DeviceGuard g(c->device);
+  HIPTRY(hipHostMalloc(out, std::max<uint64_t>(bytes, 1), hipHostMallocMapped | hipHostMallocPortable));
+  return WG_OK;
+}
+
+int wg_host_free(wg_ctx* c, void* p) {
+  if (!c) return fail(WG_EINVAL, "NULL context");
+  if (!p) return WG_OK;
+  DeviceGuard g(c->device);
+  HIPTRY(hipHostFree(p));
+  return WG_OK;
+}
+
+int wg_host_register(wg_ctx* c, void* p, uint64_t bytes) {
+  if (!c || !p || !bytes) return fail(WG_EINVAL, "NULL argument");
+  DeviceGuard g(c->device);
+  HIPTRY(hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+  return WG_OK;
+}
+
+int wg_host_unregister(wg_ctx* c, void* p) {
+  if (!c || !p) return fail(WG_EINVAL, "NULL argument");
+  DeviceGuard g(c->device);
+  HIPTRY(hipHostUnregister(p));
   return WG_OK;
 }
 

@@ -1,0 +1,42 @@
+"""Multi-GPU layout of the transport path: one process per GPU, sharded by session.
+
+Packets are independent given (key, counter), and a session's keys and
+counters never leave its owner, so the batch shards with no data-path collective:
+session s belongs to rank s mod world (the reference's sessions are likewise disjoint,
+EstablishedSession.java:59-71). The only collectives are the benchmark's timing
+barrier and the max/sum reductions of its report — on RCCL ("nccl") on the GPU box and
+on gloo in the CPU tests.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def session_shard(n_sessions: int, rank: int, world: int) -> np.ndarray:
+    """Sessions owned by `rank`: s with s mod world == rank."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"rank {rank} outside world {world}")
+    return np.arange(rank, n_sessions, world, dtype=np.int64)
+
+
+def shard_packets(total: int, n_sessions: int, rank: int, world: int):
+    """Per-rank packet columns for `total` packets spread evenly over `n_sessions`:
+    (local key slot, global session id, per-session counter) per packet. Each session
+    counts its packets from 0, as SymmetricKeypair issues counters (SymmetricKeypair.java:64)."""
+    mine = session_shard(n_sessions, rank, world)
+    per = total // n_sessions
+    slots = np.repeat(np.arange(len(mine), dtype=np.int64), per)
+    sessions = np.repeat(mine, per)
+    counters = np.tile(np.arange(per, dtype=np.uint64), len(mine))
+    return slots, sessions, counters
+
+
+def reduce_report(dist, device, elapsed: float, seal_ms: float, open_ms: float, payload: float, ok: bool):
+    """Max of the timings and sum of the payload / failures over ranks (world > 1)."""
+    import torch
+    t = torch.tensor([elapsed, seal_ms, open_ms], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    p = torch.tensor([payload, 0.0 if ok else 1.0], dtype=torch.float64, device=device)
+    dist.all_reduce(p)
+    e, s, o = t.tolist()
+    return e, s, o, p[0].item(), p[1].item() == 0.0

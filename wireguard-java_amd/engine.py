@@ -54,10 +54,14 @@ class Engine:
         self.key_slots = key_slots
         self._free = list(range(key_slots - 1, -1, -1))
         self._slot_lock = threading.Lock()
+        self._pinned = {}
 
     # ---- lifecycle --------------------------------------------------------------
     def close(self):
         if self.ctx:
+            for p in self._pinned.values():
+                self._lib.wg_host_free(self.ctx, p)
+            self._pinned.clear()
             self._lib.wg_ctx_destroy(self.ctx)
             self.ctx = None
 
@@ -122,18 +126,37 @@ class Engine:
                                         stream if stream is not None else _torch_stream()))
 
     # ---- host buffers ---------------------------------------------------------------
-    def seal_host(self, desc: np.ndarray, inp: np.ndarray, out: np.ndarray, max_len: int, uniform: bool = False):
+    def seal_host(self, desc: np.ndarray, inp, out, max_len: int, uniform: bool = False):
+        """wg_seal_host: a batch in host memory. ``inp``/``out`` are numpy arrays (pageable:
+        chunked copy pipeline) or pinned buffers from :meth:`host_alloc` (zero-copy)."""
         d = np.ascontiguousarray(desc)
-        L.check(self._lib.wg_seal_host(self.ctx, d.ctypes.data, len(d), inp.ctypes.data, inp.nbytes, out.ctypes.data,
-                                       out.nbytes, max_len, L.WG_F_UNIFORM if uniform else 0))
+        ip, isz = _host_buf(inp)
+        op, osz = _host_buf(out)
+        L.check(self._lib.wg_seal_host(self.ctx, d.ctypes.data, len(d), ip, isz, op, osz, max_len,
+                                       L.WG_F_UNIFORM if uniform else 0))
 
-    def open_host(self, desc: np.ndarray, inp: np.ndarray, out: np.ndarray, max_len: int,
-                  uniform: bool = False) -> np.ndarray:
+    def open_host(self, desc: np.ndarray, inp, out, max_len: int, uniform: bool = False) -> np.ndarray:
         d = np.ascontiguousarray(desc)
         status = np.zeros(len(d), np.uint32)
-        L.check(self._lib.wg_open_host(self.ctx, d.ctypes.data, len(d), inp.ctypes.data, inp.nbytes, out.ctypes.data,
-                                       out.nbytes, status.ctypes.data, max_len, L.WG_F_UNIFORM if uniform else 0))
+        ip, isz = _host_buf(inp)
+        op, osz = _host_buf(out)
+        L.check(self._lib.wg_open_host(self.ctx, d.ctypes.data, len(d), ip, isz, op, osz, status.ctypes.data, max_len,
+                                       L.WG_F_UNIFORM if uniform else 0))
         return status
+
+    def host_alloc(self, nbytes: int) -> np.ndarray:
+        """A pinned, device-mapped host ring (wg_host_alloc) as a uint8 numpy array; freed
+        with :meth:`host_free` (or when the engine closes)."""
+        p = ctypes.c_void_p()
+        L.check(self._lib.wg_host_alloc(self.ctx, nbytes, ctypes.byref(p)))
+        arr = np.ctypeslib.as_array((ctypes.c_uint8 * max(nbytes, 1)).from_address(p.value))[:nbytes]
+        self._pinned[arr.ctypes.data] = p
+        return arr
+
+    def host_free(self, arr: np.ndarray) -> None:
+        p = self._pinned.pop(arr.ctypes.data, None)
+        if p is not None:
+            L.check(self._lib.wg_host_free(self.ctx, p))
 
     def aead_host(self, mode: int, descs, keys: bytes, inp: bytes, aad: bytes, out_size: int):
         """General AEAD / primitive batch on host buffers (wg_aead_host). Returns (out, status)."""
@@ -194,3 +217,11 @@ def default_engine(device: int | None = None) -> Engine:
         if dev not in _default:
             _default[dev] = Engine(dev, key_slots=int(os.environ.get("WG_KEY_SLOTS", "65536")))
         return _default[dev]
+
+
+def _host_buf(x):
+    """(pointer, nbytes) of a host buffer: numpy array or CPU torch tensor (pinned or not)."""
+    if isinstance(x, np.ndarray):
+        assert x.flags.c_contiguous
+        return x.ctypes.data, x.nbytes
+    return x.data_ptr(), x.numel() * x.element_size()

@@ -98,6 +98,58 @@ public final class TransportBatch {
 		}
 	}
 
+	/**
+	 * A pinned, device-mapped host ring (wg_host_alloc): packet buffers allocated here make
+	 * {@link #sealHost} / {@link #openHost} zero-copy. Free with {@link #freeHostRing}.
+	 */
+	public static MemorySegment allocHostRing(long bytes) {
+		try (var arena = Arena.ofConfined()) {
+			var out = arena.allocate(ADDRESS);
+			WgAead.check((int) WgAead.HOST_ALLOC.invokeExact(WgAead.CTX, bytes, out));
+			return out.get(ADDRESS, 0).reinterpret(bytes);
+		} catch (RuntimeException e) {
+			throw e;
+		} catch (Throwable e) {
+			throw new RuntimeException(e);
+		}
+	}
+
+	public static void freeHostRing(MemorySegment ring) {
+		try {
+			WgAead.check((int) WgAead.HOST_FREE.invokeExact(WgAead.CTX, ring));
+		} catch (RuntimeException e) {
+			throw e;
+		} catch (Throwable e) {
+			throw new RuntimeException(e);
+		}
+	}
+
+	/** Seals a batch whose buffers are in host memory (tun ring in, UDP ring out); synchronous. */
+	public static void sealHost(MemorySegment table, int n, MemorySegment in, MemorySegment out, int maxLen,
+	                            boolean uniform) {
+		try {
+			WgAead.check((int) WgAead.SEAL_HOST.invokeExact(WgAead.CTX, table, n, in, in.byteSize(), out,
+				out.byteSize(), maxLen, uniform ? WgAead.WG_F_UNIFORM : 0));
+		} catch (RuntimeException e) {
+			throw e;
+		} catch (Throwable e) {
+			throw new RuntimeException(e);
+		}
+	}
+
+	/** Opens a host-memory batch; status (int32[n], host) gets WG_PKT_OK / WG_PKT_BADTAG per packet. */
+	public static void openHost(MemorySegment table, int n, MemorySegment in, MemorySegment out, MemorySegment status,
+	                            int maxLen, boolean uniform) {
+		try {
+			WgAead.check((int) WgAead.OPEN_HOST.invokeExact(WgAead.CTX, table, n, in, in.byteSize(), out,
+				out.byteSize(), status, maxLen, uniform ? WgAead.WG_F_UNIFORM : 0));
+		} catch (RuntimeException e) {
+			throw e;
+		} catch (Throwable e) {
+			throw new RuntimeException(e);
+		}
+	}
+
 	public static void sync(MemorySegment stream) {
 		try {
 			WgAead.check((int) WgAead.SYNC.invokeExact(WgAead.CTX, stream));

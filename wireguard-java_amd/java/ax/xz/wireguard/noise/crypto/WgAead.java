@@ -30,7 +30,7 @@ public final class WgAead {
 	public static final long AEAD_DESC_SIZE = 64, PKT_DESC_SIZE = 32;
 
 	static final MethodHandle SELFTEST, CTX_CREATE, LAST_ERROR, KEYS_SET, KEYS_ZERO, SEAL1, OPEN1, AEAD_HOST,
-		SEAL_BATCH, OPEN_BATCH, SYNC;
+		SEAL_BATCH, OPEN_BATCH, SYNC, SEAL_HOST, OPEN_HOST, HOST_ALLOC, HOST_FREE;
 
 	/** The process-wide context (one HIP device, its stream and its device key table). */
 	static final MemorySegment CTX;
@@ -57,6 +57,12 @@ public final class WgAead {
 		OPEN_BATCH = down(linker, symbols, "wg_open_batch", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT,
 			ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS, JAVA_INT, JAVA_INT, ADDRESS));
 		SYNC = down(linker, symbols, "wg_sync", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS));
+		SEAL_HOST = down(linker, symbols, "wg_seal_host", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT,
+			ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, JAVA_INT, JAVA_INT));
+		OPEN_HOST = down(linker, symbols, "wg_open_host", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT,
+			ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS, JAVA_INT, JAVA_INT));
+		HOST_ALLOC = down(linker, symbols, "wg_host_alloc", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS));
+		HOST_FREE = down(linker, symbols, "wg_host_free", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS));
 
 		int device = Integer.getInteger("wg.device", 0);
 		KEY_SLOTS = Integer.getInteger("wg.keySlots", 65536);
