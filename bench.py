@@ -47,6 +47,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = "device-resident AEAD GiB/s, 64K x 1420B seal+open, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# VALU issue peak: 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction (MI355X_MICROARCH.md)
+VALU_PEAK_WIPS = 1024 * 2.4e9 / 2
 GIB = float(1 << 30)
 
 
@@ -78,13 +80,11 @@ def build_workload(name: str, rank: int, world: int):
     if name == "c3":
         total, L, sessions = 8 * 1024 * 1024, 1420, 1024
         # session s -> GPU s mod world; each session's packets carry its own counters
-        my_sessions = np.arange(rank, sessions, world)
-        per = total // sessions
-        n = per * len(my_sessions)
-        lengths = np.full(n, L, np.int64)
-        slots = np.repeat(np.arange(len(my_sessions)), per)
-        counters = np.tile(np.arange(per, dtype=np.uint64), len(my_sessions))
-        return lengths, slots, counters, len(my_sessions), f"C3: {total} x {L}B total over {world} GPU(s), sharded by session", True
+        D = importlib.import_module("wireguard-java_amd.dist")
+        slots, _, counters = D.shard_packets(total, sessions, rank, world)
+        lengths = np.full(len(slots), L, np.int64)
+        nkeys = len(D.session_shard(sessions, rank, world))
+        return lengths, slots, counters, nkeys, f"C3: {total} x {L}B total over {world} GPU(s), sharded by session", True
     raise SystemExit(f"unknown workload {name}")
 
 
@@ -121,6 +121,19 @@ def cpu_baseline(lengths, slots, counters, keys, budget_s: float = 1.5):
             "sample": f"{n} packets of the same workload, seal+open, {reps} reps, oracle/liboracle.so "
                       f"(-O3, bit-exact restatement of the reference C path)",
             "single_thread": round(single, 3)}
+
+
+def pmc_valu_insts():
+    """SQ_INSTS_VALU per k_stream launch (mean of seal and open) from the committed PMC summary."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
+    if not files:
+        return None
+    try:
+        d = json.load(open(files[-1]))
+        v = [d[k]["counters_mean"]["SQ_INSTS_VALU"] for k in ("seal", "open") if k in d]
+        return sum(v) / len(v) if v else None
+    except Exception:
+        return None
 
 
 def pmc_traffic():
@@ -293,15 +306,9 @@ def main():
 
     payload = 2.0 * float(lengths.sum())  # sealed + opened bytes per step on this rank
     if world > 1:
-        t = torch.tensor([elapsed, seal_ms, open_ms, gpu_step_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, seal_ms, open_ms, gpu_step_ms = t.tolist()
-        p = torch.tensor([payload], dtype=torch.float64, device=dev)
-        dist.all_reduce(p)
-        payload_all = p.item()
-        okt = torch.tensor([0 if (ok_status and ok_data) else 1], dtype=torch.int32, device=dev)
-        dist.all_reduce(okt)
-        all_ok = okt.item() == 0
+        D = importlib.import_module("wireguard-java_amd.dist")
+        (elapsed, seal_ms, open_ms, gpu_step_ms), payload_all, all_ok = D.reduce_report(
+            dist, dev, [elapsed, seal_ms, open_ms, gpu_step_ms], payload, ok_status and ok_data)
     else:
         payload_all = payload
         all_ok = ok_status and ok_data
@@ -311,6 +318,7 @@ def main():
     step_alg = float((4 * lengths + 32).sum())
     achieved = step_alg / (gpu_step_ms * 1e-3) / 1e9
     traffic = pmc_traffic() if args.workload == "c1" else None
+    valu = pmc_valu_insts() if args.workload == "c1" else None
 
     if rank == 0:
         line = {
@@ -335,6 +343,11 @@ def main():
                          "open_ms": round(open_ms, 5)},
             "verified": all_ok,
         }
+        if valu:
+            rate = valu / (gpu_step_ms / 2 * 1e-3)
+            line["valu_roofline"] = {"insts_per_launch": round(valu), "achieved": round(rate / 1e12, 4),
+                                     "peak": round(VALU_PEAK_WIPS / 1e12, 4), "unit": "T wave-instr/s",
+                                     "frac": round(rate / VALU_PEAK_WIPS, 4), "source": "SQ_INSTS_VALU, profiles/pmc_*.json"}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(lengths, slots, counters, keys)
         print(json.dumps(line), flush=True)

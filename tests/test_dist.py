@@ -1,0 +1,109 @@
+"""Multi-process layout of the transport path on CPU (gloo, world_size 2): session
+sharding covers every (session, counter) exactly once, each rank's shard seals to the
+same bytes as a single-process run, and the report reductions take max/sum over ranks
+(bench.py uses the same helpers over RCCL)."""
+import hashlib
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from wgtest import ROOT, oracle, splitmix_np
+
+TOTAL, SESSIONS, L = 2048, 16, 300
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _session_digests(D, O, rank, world):
+    """Seal this rank's shard with the oracle; sha256 of every session's ct||tag stream."""
+    slots, sessions, counters = D.shard_packets(TOTAL, SESSIONS, rank, world)
+    mine = D.session_shard(SESSIONS, rank, world)
+    n = len(slots)
+    desc = np.zeros(n, O.WG_PKT)
+    desc["in_off"] = np.arange(n, dtype=np.uint64) * L
+    desc["out_off"] = np.arange(n, dtype=np.uint64) * (L + 16)
+    desc["counter"], desc["len"], desc["key_slot"] = counters, L, slots
+    keys = np.concatenate([splitmix_np(1000 + int(s), 32) for s in mine]) if len(mine) else np.zeros(32, np.uint8)
+    pt = np.concatenate([splitmix_np(5000 + int(s) * 100003 + int(c), L) for s, c in zip(sessions, counters)])
+    out = np.zeros(n * (L + 16), np.uint8)
+    O.seal_batch(desc, pt, out, keys, threads=2)
+    dig = {}
+    for s in mine:
+        idx = np.nonzero(sessions == s)[0]
+        h = hashlib.sha256()
+        for i in idx:
+            h.update(out[i * (L + 16):(i + 1) * (L + 16)].tobytes())
+        dig[int(s)] = h.hexdigest()
+    return dig, n
+
+
+def _worker(rank, world, port, q):
+    import importlib
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        D = importlib.import_module("wireguard-java_amd.dist")
+        O = oracle()
+        dig, n = _session_digests(D, O, rank, world)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, dig)
+        (t_max, s_ms, o_ms), payload, ok = D.reduce_report(dist, "cpu", [1.0 + rank, 0.5 * rank, 2.0], float(n),
+                                                           rank != 7)
+        if rank == 0:
+            merged = {}
+            for g in gathered:
+                assert not set(g) & set(merged), "a session was sealed on two ranks"
+                merged.update(g)
+            q.put((merged, t_max, s_ms, o_ms, payload, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_session_shard_partition():
+    import importlib
+    D = importlib.import_module("wireguard-java_amd.dist")
+    for world in (1, 2, 3, 8):
+        seen = np.concatenate([D.session_shard(1024, r, world) for r in range(world)])
+        assert np.array_equal(np.sort(seen), np.arange(1024))
+        pairs = set()
+        for r in range(world):
+            _, sess, ctr = D.shard_packets(8192, 1024, r, world)
+            pairs |= set(zip(sess.tolist(), ctr.tolist()))
+        assert len(pairs) == 8192
+    with pytest.raises(ValueError):
+        D.session_shard(4, 2, 2)
+
+
+def test_gloo_world2_matches_single_process():
+    import importlib
+    D = importlib.import_module("wireguard-java_amd.dist")
+    single, n1 = _session_digests(D, oracle(), 0, 1)
+    assert n1 == TOTAL
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        merged, t_max, s_ms, o_ms, payload, ok = q.get(timeout=240)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert merged == single                      # union of shards == unsharded run, byte for byte
+    assert (t_max, s_ms, o_ms) == (2.0, 0.5, 2.0)  # max over ranks
+    assert payload == TOTAL and ok               # payload summed over ranks

@@ -31,12 +31,12 @@ def shard_packets(total: int, n_sessions: int, rank: int, world: int):
     return slots, sessions, counters
 
 
-def reduce_report(dist, device, elapsed: float, seal_ms: float, open_ms: float, payload: float, ok: bool):
-    """Max of the timings and sum of the payload / failures over ranks (world > 1)."""
+def reduce_report(dist, device, timings, payload: float, ok: bool):
+    """Max of each timing and sum of the payload / failures over the ranks (world > 1).
+    Returns (timings_max, payload_sum, all_ok)."""
     import torch
-    t = torch.tensor([elapsed, seal_ms, open_ms], dtype=torch.float64, device=device)
+    t = torch.tensor(list(timings), dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     p = torch.tensor([payload, 0.0 if ok else 1.0], dtype=torch.float64, device=device)
     dist.all_reduce(p)
-    e, s, o = t.tolist()
-    return e, s, o, p[0].item(), p[1].item() == 0.0
+    return t.tolist(), p[0].item(), p[1].item() == 0.0
