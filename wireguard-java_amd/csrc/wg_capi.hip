@@ -118,6 +118,9 @@ struct Tunables {
   int use_pipe = 0;                                         // k_pipe (software-pipelined) for transport
   int use_lean = 0;                                         // k_lean (state in LDS) for transport
   uint32_t stream_lds_pad = 0;                              // dynamic LDS per wave: caps occupancy
+  int use_wave = 0;                                         // k_wave (8 waves/SIMD layout) for transport
+  int wave_variant = 3;                                     // k_wave<MODE, V, WPG> variant bits
+  int wave_wpg = 4;                                         // k_wave waves per workgroup (1, 4, 8)
   Tunables() {
     if (const char* e = getenv("WG_STREAM_LDS_PAD")) stream_lds_pad = (uint32_t)std::min(65536, std::max(0, atoi(e)));
     if (const char* e = getenv("WG_STREAM_PPW")) stream_ppw_uniform = stream_ppw_mixed = std::max(1, atoi(e));
@@ -126,7 +129,10 @@ struct Tunables {
       use_tile_for_transport = strcmp(e, "tile") == 0;
       use_pipe = strcmp(e, "pipe") == 0;
       use_lean = strcmp(e, "lean") == 0;
+      use_wave = strcmp(e, "wave") == 0;
     }
+    if (const char* e = getenv("WG_WAVE_VARIANT")) wave_variant = atoi(e) & 3;
+    if (const char* e = getenv("WG_WAVE_WPG")) wave_wpg = atoi(e) == 1 ? 1 : atoi(e) == 8 ? 8 : 4;
     if (const char* e = getenv("WG_STREAM_VARIANT")) stream_variant = atoi(e) & 63;
     if (const char* e = getenv("WG_TILE_PASSES")) tile_passes = std::min(4u, std::max(1u, (uint32_t)atoi(e)));
     if (const char* e = getenv("WG_POLY_WAVES")) poly_waves = std::min(4u, std::max(1u, (uint32_t)atoi(e)));
@@ -284,11 +290,31 @@ int launch_stream(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
   P.out_size = out_size;
   P.keys = c->keys;
   P.status = status;
+#ifdef WG_DIAG
+  P.stamps = g_stamps;
+#endif
   const uint32_t grid = (n + P.ppw - 1) / P.ppw;
   const uint32_t pad = tunables().stream_lds_pad;
   hipEvent_t ev;
   record_start(c, s, &ev);
-  if (tunables().use_lean) {
+  if (tunables().use_wave) {
+    const int G = tunables().wave_wpg, V = tunables().wave_variant;
+    const uint32_t wgrid = (grid + G - 1) / G;
+#define WG_WAVE_LAUNCH(VV, GG) hipLaunchKernelGGL((wgk::k_wave<MODE, VV, GG>), dim3(wgrid), dim3(64 * GG), 0, s, P)
+    if (G == 1) {
+      switch (V) {
+        case 0: WG_WAVE_LAUNCH(0, 1); break;
+        case 1: WG_WAVE_LAUNCH(1, 1); break;
+        case 2: WG_WAVE_LAUNCH(2, 1); break;
+        default: WG_WAVE_LAUNCH(3, 1); break;
+      }
+    } else if (G == 4) {
+      if (V & 2) WG_WAVE_LAUNCH(3, 4); else WG_WAVE_LAUNCH(1, 4);
+    } else {
+      if (V & 2) WG_WAVE_LAUNCH(3, 8); else WG_WAVE_LAUNCH(1, 8);
+    }
+#undef WG_WAVE_LAUNCH
+  } else if (tunables().use_lean) {
     hipLaunchKernelGGL((wgk::k_lean<MODE>), dim3(grid), dim3(64), 0, s, P);
   } else if (tunables().use_pipe) {
     hipLaunchKernelGGL((wgk::k_pipe<MODE, 0>), dim3(grid), dim3(64), 0, s, P);

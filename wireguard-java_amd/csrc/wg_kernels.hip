@@ -541,7 +541,33 @@ struct StreamParams {
   uint64_t out_size;
   const uint32_t* keys;
   uint32_t* status;
+  uint64_t* stamps;  // WG_DIAG builds only: 8 x u64 per wave
 };
+
+// Per-wave phase accounting for k_stream (diagnostic library only): cycles spent
+// starting packets, in ChaCha, in Poly1305 and finishing, plus realtime start/end.
+#ifdef WG_DIAG
+#define WG_PH_DECL uint64_t ph_t = 0, ph_acc[4] = {0, 0, 0, 0}; const uint64_t ph_r0 = __builtin_amdgcn_s_memrealtime();
+#define WG_PH_MARK() do { asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ph_t)::"memory"); } while (0)
+#define WG_PH_ADD(k) do { uint64_t n_; asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(n_)::"memory"); ph_acc[k] += n_ - ph_t; ph_t = n_; } while (0)
+#define WG_PH_STORE()                                                                             \
+  do {                                                                                            \
+    if (P.stamps && threadIdx.x == 0) {                                                           \
+      uint64_t* o_ = P.stamps + (size_t)blockIdx.x * 8;                                           \
+      o_[0] = ph_r0; o_[1] = __builtin_amdgcn_s_memrealtime();                                    \
+      o_[2] = ph_acc[0]; o_[3] = ph_acc[1]; o_[4] = ph_acc[2]; o_[5] = ph_acc[3];                 \
+      uint32_t hw_, xcc_;                                                                         \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));                           \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));                         \
+      o_[6] = hw_; o_[7] = xcc_;                                                                  \
+    }                                                                                             \
+  } while (0)
+#else
+#define WG_PH_DECL
+#define WG_PH_MARK() do {} while (0)
+#define WG_PH_ADD(k) do {} while (0)
+#define WG_PH_STORE() do {} while (0)
+#endif
 
 // V (variant bits, for A/B builds; bits 4/5 are timing ablations that skip Poly1305 / the keystream): bit3 ILP form of the Poly1305 multiply, bit0 prefetch payload before the rounds,
 // bit1 re-read the key from LDS for the feed-forward, bit2 cap VGPRs for 8 waves/SIMD
@@ -565,8 +591,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((V & 4)
   uint32_t len = 0, ctr_lo = 0, ctr_hi = 0, nb = 0, nc = 0, D = 0;
   bool valid = false;
   uint32_t acc[5];
+  WG_PH_DECL
 
   while (__any(have)) {
+    WG_PH_MARK();
     if (have && round == 0) {  // start a packet: descriptor, bounds, key
       const uint4* dp = (const uint4*)(P.desc + pkt);
       const uint4 lo = dp[0], hi = dp[1];
@@ -591,6 +619,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((V & 4)
       }
     }
     __syncthreads();  // one wave per workgroup: orders the slot key writes
+    WG_PH_ADD(0);
 
     // ---- ChaCha20: block b of the slot's packet ------------------------------------
     const uint32_t b = 8u * round + j;
@@ -631,6 +660,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((V & 4)
       }
     }
     __syncthreads();
+    WG_PH_ADD(1);
 
     // ---- Poly1305 ------------------------------------------------------------------
     if (!(V & 16) && have && valid) {
@@ -687,6 +717,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((V & 4)
       }
     }
 
+    WG_PH_ADD(2);
     // ---- finish packets whose last round this was ------------------------------------
     const bool done = have && (!valid || 8u * (round + 1u) >= nb);
     if (done) {
@@ -747,7 +778,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((V & 4)
       ++round;
     }
     next += (uint32_t)__popcll(fin);
+    WG_PH_ADD(3);
   }
+  WG_PH_STORE();
 }
 
 // ---------------------------------------------------------------------------
@@ -1272,6 +1305,241 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) k_
 }
 
 // explicit instantiations used by wg_capi.hip
+// ---------------------------------------------------------------------------
+// k_wave — k_stream's slot/round algorithm laid out for 8 waves per SIMD:
+// <= 64 VGPRs and 5024 B of LDS per wave (160 KB / 5 KB = 32 waves per CU).
+//  * lane-derived values (slot, lane in slot, LDS addresses, shuffle sources) come
+//    from an opaque copy of threadIdx.x in each phase, so the compiler recomputes
+//    them (1-3 VALU) instead of keeping ~25 hoisted constants live across the rounds;
+//  * the packet record (offsets, counter, length, validity) lives in LDS and is
+//    re-read where needed; the ChaCha key is re-read for the feed-forward;
+//  * W = r^(8-j) stays in 5 VGPRs (k_stream kept it in 1.25 KB of LDS); only
+//    R = r^8 is stored, 5R is formed on the fly;
+//  * the Poly1305 step per round is 4 predicated chunk steps at constant LDS
+//    offsets: chunk c of the slot's round image sits at img[4 sbase + 4 - 32 round + c].
+//  * WPG independent waves share a workgroup (each with its own LDS arrays, no
+//    block barriers): one-wave workgroups are dispatched at only ~1 per 11 cycles
+//    chip-wide, which left a 65536-packet launch with ~40% of its wave slots empty.
+// Results are identical to k_stream (same Horner order, same finish).
+__device__ __forceinline__ uint32_t opaque_lane() {
+  uint32_t x = threadIdx.x & 63u;
+  asm volatile("" : "+v"(x));
+  return x;
+}
+// orders this wave's LDS writes before its other lanes' reads (LDS is in order per wave)
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <int MODE, int V, int WPG>
+__global__ void __launch_bounds__(64 * WPG) __attribute__((amdgpu_waves_per_eu((V & 2) ? 8 : 1)))
+k_wave(StreamParams P) {
+  static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
+  __shared__ uint4 img_[WPG][8 * 8 * 4];  // 4096 B per wave: [slot][lane][4 chunks], the round's MAC input
+  __shared__ uint4 skey_[WPG][8 * 2];     // 256 B: slot ChaCha key
+  __shared__ uint4 sotk_[WPG][8 * 2];     // 256 B: slot Poly1305 one-time key r || s
+  __shared__ uint4 srec_[WPG][8 * 2];     // 256 B: {in_off, out_off} {ctr lo, ctr hi, len, valid}
+  __shared__ uint32_t spow_[WPG][8 * 5];  // 160 B: R = r^8 limbs
+  const uint32_t wv = WPG == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint4* const img = img_[wv];
+  uint4* const skey = skey_[wv];
+  uint4* const sotk = sotk_[wv];
+  uint4* const srec = srec_[wv];
+  uint32_t* const spow = spow_[wv];
+  const uint32_t w0 = (blockIdx.x * WPG + wv) * P.ppw, w1 = min(P.n, w0 + P.ppw);
+  uint32_t next = w0 + SLOT_LANES;  // wave-uniform
+  uint32_t pkt = w0 + (opaque_lane() >> 3);
+  bool have = pkt < w1;
+  uint32_t round = 0;
+  uint32_t acc[5], W[5];
+
+  while (__any(have)) {
+    if (have && round == 0) {  // start a packet: lane 0 of the slot fills the record
+      const uint32_t lane = opaque_lane(), s = lane >> 3;
+      if ((lane & 7u) == 0) {
+        const uint4* dp = (const uint4*)(P.desc + pkt);
+        const uint4 lo = dp[0], hi = dp[1];
+        const uint64_t in_off = (uint64_t)lo.x | ((uint64_t)lo.y << 32);
+        const uint64_t out_off = (uint64_t)lo.z | ((uint64_t)lo.w << 32);
+        const uint32_t len = hi.z, ks_ = hi.w;
+        bool valid = len <= P.max_len && ks_ < P.key_slots;
+        const uint64_t in_need = (uint64_t)len + (MODE == WG_MODE_OPEN ? 16u : 0u);
+        const uint64_t out_need = (uint64_t)len + (MODE == WG_MODE_SEAL ? 16u : 0u);
+        valid = valid && in_off <= P.in_size && in_need <= P.in_size - in_off;
+        valid = valid && out_off <= P.out_size && out_need <= P.out_size - out_off;
+        srec[2 * s] = lo;
+        srec[2 * s + 1] = make_uint4(hi.x, hi.y, len, valid ? 1u : 0u);
+        if (valid) {
+          const uint4* kp = (const uint4*)(P.keys + 8u * ks_);
+          skey[2 * s] = kp[0];
+          skey[2 * s + 1] = kp[1];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 5; ++i) acc[i] = 0;
+    }
+    wave_lds_sync();  // the record writes before the slot's other lanes read them
+
+    // ---- ChaCha20: block b = 8 round + j of the slot's packet ----------------------
+    {
+      const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
+      const uint4 rc = srec[2 * s + 1];
+      const uint32_t len = rc.z;
+      const uint32_t nb = ((len + 63u) >> 6) + 1u;
+      const uint32_t b = 8u * round + j;
+      const bool act = have && rc.w && b < nb;
+      const bool data = act && b > 0;
+      const uint32_t off = 64u * (b - 1u);
+      const uint32_t nbytes = data ? min(64u, len - off) : 0u;
+      uint32_t w[16];
+      if ((V & 1) && data) {
+        const uint4 ro = srec[2 * s];
+        load_block(P.in + ((uint64_t)ro.x | ((uint64_t)ro.y << 32)) + off, nbytes, w);
+      }
+      if (act) {
+        uint32_t ks[16];
+        chacha20_block_lds(&skey[2 * s], b, rc.x, rc.y, 0u, ks);
+        if (!data) {
+          sotk[2 * s] = make_uint4(ks[0], ks[1], ks[2], ks[3]);
+          sotk[2 * s + 1] = make_uint4(ks[4], ks[5], ks[6], ks[7]);
+        } else {
+          const uint4 ro = srec[2 * s];
+          if (!(V & 1)) load_block(P.in + ((uint64_t)ro.x | ((uint64_t)ro.y << 32)) + off, nbytes, w);
+          if constexpr (MODE == WG_MODE_OPEN) {
+            if (nbytes < 64u) mask_block(nbytes, w);
+            lds_store_block((uint8_t*)&img[4 * lane], w);
+          }
+#pragma unroll
+          for (int i = 0; i < 16; ++i) w[i] ^= ks[i];
+          store_block(P.out + ((uint64_t)ro.z | ((uint64_t)ro.w << 32)) + off, nbytes, w);
+          if constexpr (MODE == WG_MODE_SEAL) {
+            if (nbytes < 64u) mask_block(nbytes, w);
+            lds_store_block((uint8_t*)&img[4 * lane], w);
+          }
+        }
+      }
+    }
+    wave_lds_sync();
+
+    // ---- Poly1305 over this round's chunks ------------------------------------------
+    const uint4 rc = srec[2 * (opaque_lane() >> 3) + 1];
+    const bool valid = rc.w != 0;
+    const uint32_t len = rc.z, nb = ((len + 63u) >> 6) + 1u, nc = (len + 15u) >> 4;
+    if (have && valid) {
+      const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u, sbase = lane & ~7u;
+      if (round == 0) {  // r and its powers: lane j gets r^(j+1); R = r^8, W = r^(8-j)
+        const uint4 o = sotk[2 * s];
+        uint32_t x[5];
+        poly_r_limbs(o.x, o.y, o.z, o.w, x);
+#pragma unroll
+        for (uint32_t st = 1; st < 8u; st <<= 1) {
+          uint32_t y[5], ys[5];
+          shfl5(x, (int)(j >= st ? lane - st : lane), y);
+          poly_scale5(y, ys);
+          if (j >= st) poly_mul(x, y, ys);
+        }
+        shfl5(x, (int)(sbase + 7u - j), W);
+        if (j == 7u) {
+#pragma unroll
+          for (int i = 0; i < 5; ++i) spow[5 * s + i] = x[i];
+        }
+      }
+      uint32_t R[5], Rs[5];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) R[i] = spow[5 * s + i];
+      poly_scale5(R, Rs);
+      const uint32_t M = nc + 1u, D = 8u * ((M + 7u) >> 3) - M;
+      const uint32_t c_lo = round ? 32u * round - 4u : 0u;
+      const uint32_t c_end = min(nc, 32u * round + 28u);
+      const uint32_t c0 = c_lo + ((j - ((c_lo + D) & 7u)) & 7u);
+      const uint4* ip = &img[4u * sbase + 4u - 32u * round + c0];
+#pragma unroll
+      for (uint32_t t = 0; t < 4u; ++t) {
+        if (c0 + 8u * t < c_end) {
+          const uint4 v = ip[8u * t];
+          poly_mul(acc, R, Rs);
+          uint32_t cl[5];
+          poly_block_limbs(v.x, v.y, v.z, v.w, 1u << 24, cl);
+#pragma unroll
+          for (int i = 0; i < 5; ++i) acc[i] += cl[i];
+        }
+      }
+    }
+
+    // ---- finish packets whose last round this was ------------------------------------
+    const bool done = have && (!valid || 8u * (round + 1u) >= nb);
+    if (done) {
+      const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u, sbase = lane & ~7u;
+      if (valid) {
+        if (j == 7u) {  // the length block le64(0) || le64(len) is lane 7's last position
+          uint32_t R[5], Rs[5];
+#pragma unroll
+          for (int i = 0; i < 5; ++i) R[i] = spow[5 * s + i];
+          poly_scale5(R, Rs);
+          poly_mul(acc, R, Rs);
+          acc[2] += (len << 12) & M26;  // le64(len) sits at bit 64: limb 2 = bits 52..77
+          acc[3] += len >> 14;
+          acc[4] += 1u << 24;
+        }
+        uint32_t Ws[5];
+        poly_scale5(W, Ws);
+        poly_mul(acc, W, Ws);
+#pragma unroll
+        for (uint32_t st = 1; st < 8u; st <<= 1) {
+          uint32_t y[5];
+          shfl5(acc, (int)(j + st < 8u ? lane + st : lane), y);
+          if (j + st < 8u) {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) acc[i] += y[i];
+          }
+        }
+      }
+      uint32_t bad = valid ? 0u : 1u;
+      if (j == 0 && valid) {
+        const uint4 sv = sotk[2 * s + 1];
+        uint32_t tag[4];
+        poly_finish(acc, sv.x, sv.y, sv.z, sv.w, tag);
+        const uint4 ro = srec[2 * s];
+        if constexpr (MODE == WG_MODE_SEAL) {
+          uint8_t* tp = P.out + ((uint64_t)ro.z | ((uint64_t)ro.w << 32)) + len;
+          if ((((uintptr_t)tp) & 15u) == 0) {
+            *(uint4*)tp = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) store_u32_any(tp + 4 * i, tag[i]);
+          }
+        } else {  // all 16 bytes compared, no early exit
+          const uint8_t* tp = P.in + ((uint64_t)ro.x | ((uint64_t)ro.y << 32)) + len;
+          uint32_t diff = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) diff |= load_u32_any(tp + 4 * i) ^ tag[i];
+          bad = diff ? 1u : 0u;
+        }
+      }
+      if constexpr (MODE == WG_MODE_OPEN) {
+        bad = __shfl(bad, (int)sbase, 64);
+        if (j == 0 && P.status) P.status[pkt] = bad ? WG_PKT_BADTAG : WG_PKT_OK;
+        if (bad && valid) {  // scrub the unauthenticated plaintext written this call
+          const uint4 ro = srec[2 * s];
+          uint8_t* o = P.out + ((uint64_t)ro.z | ((uint64_t)ro.w << 32));
+          for (uint32_t i = j; i < len; i += 8u) o[i] = 0;
+        }
+      }
+    }
+    // hand the wave's next packets to the slots that finished (ballot rank)
+    const unsigned long long fin = __ballot(done && (opaque_lane() & 7u) == 0);
+    if (done) {
+      const uint32_t sbase = opaque_lane() & ~7u;
+      const uint32_t rank = (uint32_t)__popcll(fin & ((1ull << sbase) - 1ull));
+      pkt = next + rank;
+      have = pkt < w1;
+      round = 0;
+    } else if (have) {
+      ++round;
+    }
+    next += (uint32_t)__popcll(fin);
+    wave_lds_sync();  // the next packet's record overwrites this one's
+  }
+}
+
 template __global__ void k_tile<WG_MODE_SEAL, false>(TileParams);
 template __global__ void k_tile<WG_MODE_OPEN, false>(TileParams);
 template __global__ void k_tile<WG_MODE_SEAL, true>(TileParams);
@@ -1290,6 +1558,11 @@ template __global__ void k_plan_count<WG_MODE_MAC, true>(const void*, uint32_t, 
 WG_STREAM_INST(0) WG_STREAM_INST(1) WG_STREAM_INST(2) WG_STREAM_INST(3)
 WG_STREAM_INST(4) WG_STREAM_INST(5) WG_STREAM_INST(6) WG_STREAM_INST(7)
 WG_STREAM_INST(9) WG_STREAM_INST(11) WG_STREAM_INST(15) WG_STREAM_INST(17) WG_STREAM_INST(33) WG_STREAM_INST(49)
+#define WG_WAVE_INST(V, G)                                                \
+  template __global__ void k_wave<WG_MODE_SEAL, V, G>(StreamParams); \
+  template __global__ void k_wave<WG_MODE_OPEN, V, G>(StreamParams);
+WG_WAVE_INST(0, 1) WG_WAVE_INST(1, 1) WG_WAVE_INST(2, 1) WG_WAVE_INST(3, 1)
+WG_WAVE_INST(1, 4) WG_WAVE_INST(3, 4) WG_WAVE_INST(1, 8) WG_WAVE_INST(3, 8)
 template __global__ void k_lean<WG_MODE_SEAL>(StreamParams);
 template __global__ void k_lean<WG_MODE_OPEN>(StreamParams);
 template __global__ void k_pipe<WG_MODE_SEAL, 0>(StreamParams);
