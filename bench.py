@@ -336,7 +336,7 @@ def main():
             "data": "synthetic (random payload in HBM, splitmix64 keys, sequential counters)",
             "config": {"workload": wdesc, "packets_per_gpu": n, "payload_bytes": int(lengths.mean()),
                        "sessions_per_gpu": nkeys, "parallelism": f"dp{world} sharded by session, no collective"},
-            "roofline": {"bound": "hbm", "kernel": "k_stream<SEAL|OPEN>", "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": "k_wave<SEAL|OPEN>", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "alg_bytes_per_launch": int(step_alg / 2),
                          "kernel_ms": round(gpu_step_ms / 2, 5), "seal_ms": round(seal_ms, 5),

@@ -11,11 +11,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 wg = importlib.import_module("wireguard-java_amd")
 E = importlib.import_module("wireguard-java_amd.engine")
 n, L, S = int(os.environ.get("N", 65536)), int(os.environ.get("L", 1420)), 1440
-eng = wg.Engine(0, key_slots=4)
-eng.set_keys(0, bytes(range(32)) * 4)
+NK = int(os.environ.get("NKEYS", 1))
+eng = wg.Engine(0, key_slots=max(NK, 4))
+eng.set_keys(0, np.random.default_rng(1).integers(0, 256, 32 * max(NK, 4), dtype=np.uint8).tobytes())
 dev = torch.device("cuda", 0)
 off = np.arange(n, dtype=np.uint64) * S
-tdesc = torch.from_numpy(E.desc_as_int64(wg.pack_desc(off, off, np.arange(n, dtype=np.uint64), np.full(n, L), 0))).to(dev)
+tdesc = torch.from_numpy(E.desc_as_int64(wg.pack_desc(off, off, np.arange(n, dtype=np.uint64), np.full(n, L),
+                                                      np.arange(n) % NK))).to(dev)
 g = np.zeros(n, E.WG_AEAD_DTYPE)
 g["in_off"] = g["out_off"] = off
 g["len"] = L

@@ -15,11 +15,12 @@ E = importlib.import_module("wireguard-java_amd.engine")
 lib = wg.lib()
 lib.wg_diag_stamps.argtypes = [ctypes.c_void_p]
 n, L, S = int(os.environ.get("N", 65536)), int(os.environ.get("L", 1420)), 1440
-eng = wg.Engine(0, key_slots=4)
-eng.set_keys(0, bytes(range(32)))
+NK = int(os.environ.get("NKEYS", 1))
+eng = wg.Engine(0, key_slots=max(NK, 4))
+eng.set_keys(0, bytes(range(32)) * max(NK, 4))
 dev = torch.device("cuda", 0)
 off = np.arange(n, dtype=np.uint64) * S
-tdesc = torch.from_numpy(E.desc_as_int64(wg.pack_desc(off, off, np.arange(n, dtype=np.uint64), np.full(n, L), 0))).to(dev)
+tdesc = torch.from_numpy(E.desc_as_int64(wg.pack_desc(off, off, np.arange(n, dtype=np.uint64), np.full(n, L), np.arange(n) % NK))).to(dev)
 buf = torch.randint(0, 256, (n * S,), dtype=torch.uint8, device=dev)
 out = torch.zeros_like(buf)
 waves = (n + 7) // 8
@@ -51,3 +52,20 @@ print("  cycles/wave: " + "  ".join(f"{nm} {ph[:, i].mean():.0f} ({ph[:, i].mean
 edges = np.linspace(0, en.max(), 21)
 conc = [((st <= m) & (en > m)).sum() for m in (edges[:-1] + edges[1:]) / 2]
 print("  resident waves over time:", conc)
+# where did the waves run: (XCC, SE, CU, SIMD) from HW_ID / XCC_ID
+hw, xcc = s[:, 6].astype(np.int64), s[:, 7].astype(np.int64) & 0xF
+simd = (hw >> 4) & 3
+cu = (hw >> 8) & 0xF
+se = (hw >> 13) & 0x7
+key = ((xcc * 8 + se) * 16 + cu) * 4 + simd
+u, inv = np.unique(key, return_inverse=True)
+per = np.bincount(inv)
+first = np.array([(st[inv == i] < 1.0).sum() for i in range(len(u))])
+last_end = np.array([en[inv == i].max() for i in range(len(u))])
+busy = np.array([life[inv == i].sum() for i in range(len(u))])
+print(f"  SIMDs used {len(u)}; waves per SIMD min/mean/max {per.min()}/{per.mean():.1f}/{per.max()}; "
+      f"started in first 1us per SIMD min/mean/max {first.min()}/{first.mean():.1f}/{first.max()}")
+print(f"  per-SIMD last wave end (us) p0/p10/p50/p90/p100: "
+      + "/".join(f"{np.percentile(last_end, p):.1f}" for p in (0, 10, 50, 90, 100)))
+cus = np.unique(key // 4)
+print(f"  CUs used {len(cus)}; XCCs {np.unique(xcc).tolist()}; waves per XCC {np.bincount(xcc, minlength=8).tolist()}")

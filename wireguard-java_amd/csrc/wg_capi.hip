@@ -118,9 +118,9 @@ struct Tunables {
   int use_pipe = 0;                                         // k_pipe (software-pipelined) for transport
   int use_lean = 0;                                         // k_lean (state in LDS) for transport
   uint32_t stream_lds_pad = 0;                              // dynamic LDS per wave: caps occupancy
-  int use_wave = 0;                                         // k_wave (8 waves/SIMD layout) for transport
-  int wave_variant = 3;                                     // k_wave<MODE, V, WPG> variant bits
-  int wave_wpg = 4;                                         // k_wave waves per workgroup (1, 4, 8)
+  int use_wave = 1;                                         // k_wave (8 waves/SIMD layout): the default
+  int wave_variant = 5;                                     // k_wave<MODE, V, WPG>: prefetch + progress priority
+  int wave_wpg = 1;                                         // k_wave waves per workgroup (1, 4, 8)
   Tunables() {
     if (const char* e = getenv("WG_STREAM_LDS_PAD")) stream_lds_pad = (uint32_t)std::min(65536, std::max(0, atoi(e)));
     if (const char* e = getenv("WG_STREAM_PPW")) stream_ppw_uniform = stream_ppw_mixed = std::max(1, atoi(e));
@@ -129,11 +129,11 @@ struct Tunables {
       use_tile_for_transport = strcmp(e, "tile") == 0;
       use_pipe = strcmp(e, "pipe") == 0;
       use_lean = strcmp(e, "lean") == 0;
-      use_wave = strcmp(e, "wave") == 0;
+      use_wave = strcmp(e, "wave") == 0 || strcmp(e, "default") == 0;
     }
-    if (const char* e = getenv("WG_WAVE_VARIANT")) wave_variant = atoi(e) & 3;
-    if (const char* e = getenv("WG_WAVE_WPG")) wave_wpg = atoi(e) == 1 ? 1 : atoi(e) == 8 ? 8 : 4;
-    if (const char* e = getenv("WG_STREAM_VARIANT")) stream_variant = atoi(e) & 63;
+    if (const char* e = getenv("WG_WAVE_VARIANT")) wave_variant = atoi(e) & 15;
+    if (const char* e = getenv("WG_WAVE_WPG")) wave_wpg = atoi(e) == 4 ? 4 : atoi(e) == 8 ? 8 : 1;
+    if (const char* e = getenv("WG_STREAM_VARIANT")) stream_variant = atoi(e) & 127;
     if (const char* e = getenv("WG_TILE_PASSES")) tile_passes = std::min(4u, std::max(1u, (uint32_t)atoi(e)));
     if (const char* e = getenv("WG_POLY_WAVES")) poly_waves = std::min(4u, std::max(1u, (uint32_t)atoi(e)));
     if (const char* e = getenv("WG_POLY_GMAX")) poly_gmax = std::min(64u, std::max(1u, (uint32_t)atoi(e)));
@@ -306,10 +306,14 @@ int launch_stream(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
         case 0: WG_WAVE_LAUNCH(0, 1); break;
         case 1: WG_WAVE_LAUNCH(1, 1); break;
         case 2: WG_WAVE_LAUNCH(2, 1); break;
+        case 5: WG_WAVE_LAUNCH(5, 1); break;
+        case 7: WG_WAVE_LAUNCH(7, 1); break;
+        case 13: WG_WAVE_LAUNCH(13, 1); break;
+        case 15: WG_WAVE_LAUNCH(15, 1); break;
         default: WG_WAVE_LAUNCH(3, 1); break;
       }
     } else if (G == 4) {
-      if (V & 2) WG_WAVE_LAUNCH(3, 4); else WG_WAVE_LAUNCH(1, 4);
+      if (V == 15) WG_WAVE_LAUNCH(15, 4); else if (V & 2) WG_WAVE_LAUNCH(3, 4); else WG_WAVE_LAUNCH(1, 4);
     } else {
       if (V & 2) WG_WAVE_LAUNCH(3, 8); else WG_WAVE_LAUNCH(1, 8);
     }
@@ -322,7 +326,7 @@ int launch_stream(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
 #define WG_CASE(V) \
   case V: hipLaunchKernelGGL((wgk::k_stream<MODE, V>), dim3(grid), dim3(64), pad, s, P); break;
     WG_CASE(0) WG_CASE(1) WG_CASE(2) WG_CASE(3) WG_CASE(4) WG_CASE(5) WG_CASE(6) WG_CASE(7)
-    WG_CASE(9) WG_CASE(11) WG_CASE(15) WG_CASE(17) WG_CASE(33) WG_CASE(49)
+    WG_CASE(9) WG_CASE(11) WG_CASE(15) WG_CASE(17) WG_CASE(33) WG_CASE(49) WG_CASE(65) WG_CASE(73)
     default: return fail(WG_EINVAL, "WG_STREAM_VARIANT %d not built", tunables().stream_variant);
 #undef WG_CASE
   }

@@ -562,12 +562,35 @@ struct StreamParams {
       o_[6] = hw_; o_[7] = xcc_;                                                                  \
     }                                                                                             \
   } while (0)
+#define WG_PH_STORE_WAVE(idx)                                                                     \
+  do {                                                                                            \
+    if (P.stamps && (threadIdx.x & 63u) == 0) {                                                   \
+      uint64_t* o_ = P.stamps + (size_t)(idx) * 8;                                                \
+      o_[0] = ph_r0; o_[1] = __builtin_amdgcn_s_memrealtime();                                    \
+      o_[2] = ph_acc[0]; o_[3] = ph_acc[1]; o_[4] = ph_acc[2]; o_[5] = ph_acc[3];                 \
+      uint32_t hw_, xcc_;                                                                         \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));                           \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));                         \
+      o_[6] = hw_; o_[7] = xcc_;                                                                  \
+    }                                                                                             \
+  } while (0)
 #else
+#define WG_PH_STORE_WAVE(idx) do {} while (0)
 #define WG_PH_DECL
 #define WG_PH_MARK() do {} while (0)
 #define WG_PH_ADD(k) do {} while (0)
 #define WG_PH_STORE() do {} while (0)
 #endif
+
+// Progress-based wave priority: a wave drops its issue priority as it completes
+// rounds (3, 2, 1, then 0), so the SIMD's oldest-first arbitration no longer lets
+// one wave run ahead while the others idle at the end of a launch.
+__device__ __forceinline__ void progress_prio(uint32_t done_rounds) {
+  if (done_rounds == 0) __builtin_amdgcn_s_setprio(3);
+  else if (done_rounds == 1) __builtin_amdgcn_s_setprio(2);
+  else if (done_rounds == 2) __builtin_amdgcn_s_setprio(1);
+  else if (done_rounds == 3) __builtin_amdgcn_s_setprio(0);
+}
 
 // V (variant bits, for A/B builds; bits 4/5 are timing ablations that skip Poly1305 / the keystream): bit3 ILP form of the Poly1305 multiply, bit0 prefetch payload before the rounds,
 // bit1 re-read the key from LDS for the feed-forward, bit2 cap VGPRs for 8 waves/SIMD
@@ -592,8 +615,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu((V & 4)
   bool valid = false;
   uint32_t acc[5];
   WG_PH_DECL
+  uint32_t wave_rounds = 0;  // wave-uniform
 
   while (__any(have)) {
+    if constexpr ((V & 64) != 0) progress_prio(wave_rounds++);
     WG_PH_MARK();
     if (have && round == 0) {  // start a packet: descriptor, bounds, key
       const uint4* dp = (const uint4*)(P.desc + pkt);
@@ -1350,11 +1375,16 @@ k_wave(StreamParams P) {
   bool have = pkt < w1;
   uint32_t round = 0;
   uint32_t acc[5], W[5];
+  WG_PH_DECL
+  uint32_t wave_rounds = 0;  // wave-uniform
 
   while (__any(have)) {
+    if constexpr ((V & 4) != 0) progress_prio(wave_rounds++);
+    WG_PH_MARK();
+    uint32_t w[16];
     if (have && round == 0) {  // start a packet: lane 0 of the slot fills the record
-      const uint32_t lane = opaque_lane(), s = lane >> 3;
-      if ((lane & 7u) == 0) {
+      const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
+      if ((V & 8) || j == 0) {  // V & 8: every lane reads the descriptor (one coalesced request)
         const uint4* dp = (const uint4*)(P.desc + pkt);
         const uint4 lo = dp[0], hi = dp[1];
         const uint64_t in_off = (uint64_t)lo.x | ((uint64_t)lo.y << 32);
@@ -1365,18 +1395,26 @@ k_wave(StreamParams P) {
         const uint64_t out_need = (uint64_t)len + (MODE == WG_MODE_SEAL ? 16u : 0u);
         valid = valid && in_off <= P.in_size && in_need <= P.in_size - in_off;
         valid = valid && out_off <= P.out_size && out_need <= P.out_size - out_off;
-        srec[2 * s] = lo;
-        srec[2 * s + 1] = make_uint4(hi.x, hi.y, len, valid ? 1u : 0u);
-        if (valid) {
-          const uint4* kp = (const uint4*)(P.keys + 8u * ks_);
-          skey[2 * s] = kp[0];
-          skey[2 * s + 1] = kp[1];
+        if constexpr ((V & 8) != 0) {
+          // round 0's payload is requested now, in parallel with lane 0's key fetch
+          const uint32_t nbk = ((len + 63u) >> 6) + 1u;
+          if (valid && j > 0 && j < nbk) load_block(P.in + in_off + 64u * (j - 1u), min(64u, len - 64u * (j - 1u)), w);
+        }
+        if (j == 0) {
+          srec[2 * s] = lo;
+          srec[2 * s + 1] = make_uint4(hi.x, hi.y, len, valid ? 1u : 0u);
+          if (valid) {
+            const uint4* kp = (const uint4*)(P.keys + 8u * ks_);
+            skey[2 * s] = kp[0];
+            skey[2 * s + 1] = kp[1];
+          }
         }
       }
 #pragma unroll
       for (int i = 0; i < 5; ++i) acc[i] = 0;
     }
     wave_lds_sync();  // the record writes before the slot's other lanes read them
+    WG_PH_ADD(0);
 
     // ---- ChaCha20: block b = 8 round + j of the slot's packet ----------------------
     {
@@ -1389,8 +1427,8 @@ k_wave(StreamParams P) {
       const bool data = act && b > 0;
       const uint32_t off = 64u * (b - 1u);
       const uint32_t nbytes = data ? min(64u, len - off) : 0u;
-      uint32_t w[16];
-      if ((V & 1) && data) {
+      const bool prefetched = (V & 8) && round == 0;
+      if ((V & 1) && data && !prefetched) {
         const uint4 ro = srec[2 * s];
         load_block(P.in + ((uint64_t)ro.x | ((uint64_t)ro.y << 32)) + off, nbytes, w);
       }
@@ -1402,7 +1440,7 @@ k_wave(StreamParams P) {
           sotk[2 * s + 1] = make_uint4(ks[4], ks[5], ks[6], ks[7]);
         } else {
           const uint4 ro = srec[2 * s];
-          if (!(V & 1)) load_block(P.in + ((uint64_t)ro.x | ((uint64_t)ro.y << 32)) + off, nbytes, w);
+          if (!(V & 1) && !prefetched) load_block(P.in + ((uint64_t)ro.x | ((uint64_t)ro.y << 32)) + off, nbytes, w);
           if constexpr (MODE == WG_MODE_OPEN) {
             if (nbytes < 64u) mask_block(nbytes, w);
             lds_store_block((uint8_t*)&img[4 * lane], w);
@@ -1418,6 +1456,7 @@ k_wave(StreamParams P) {
       }
     }
     wave_lds_sync();
+    WG_PH_ADD(1);
 
     // ---- Poly1305 over this round's chunks ------------------------------------------
     const uint4 rc = srec[2 * (opaque_lane() >> 3) + 1];
@@ -1464,6 +1503,7 @@ k_wave(StreamParams P) {
       }
     }
 
+    WG_PH_ADD(2);
     // ---- finish packets whose last round this was ------------------------------------
     const bool done = have && (!valid || 8u * (round + 1u) >= nb);
     if (done) {
@@ -1537,7 +1577,9 @@ k_wave(StreamParams P) {
     }
     next += (uint32_t)__popcll(fin);
     wave_lds_sync();  // the next packet's record overwrites this one's
+    WG_PH_ADD(3);
   }
+  WG_PH_STORE_WAVE(blockIdx.x * WPG + wv);
 }
 
 template __global__ void k_tile<WG_MODE_SEAL, false>(TileParams);
@@ -1558,11 +1600,13 @@ template __global__ void k_plan_count<WG_MODE_MAC, true>(const void*, uint32_t, 
 WG_STREAM_INST(0) WG_STREAM_INST(1) WG_STREAM_INST(2) WG_STREAM_INST(3)
 WG_STREAM_INST(4) WG_STREAM_INST(5) WG_STREAM_INST(6) WG_STREAM_INST(7)
 WG_STREAM_INST(9) WG_STREAM_INST(11) WG_STREAM_INST(15) WG_STREAM_INST(17) WG_STREAM_INST(33) WG_STREAM_INST(49)
+WG_STREAM_INST(65) WG_STREAM_INST(73)
 #define WG_WAVE_INST(V, G)                                                \
   template __global__ void k_wave<WG_MODE_SEAL, V, G>(StreamParams); \
   template __global__ void k_wave<WG_MODE_OPEN, V, G>(StreamParams);
 WG_WAVE_INST(0, 1) WG_WAVE_INST(1, 1) WG_WAVE_INST(2, 1) WG_WAVE_INST(3, 1)
 WG_WAVE_INST(1, 4) WG_WAVE_INST(3, 4) WG_WAVE_INST(1, 8) WG_WAVE_INST(3, 8)
+WG_WAVE_INST(5, 1) WG_WAVE_INST(7, 1) WG_WAVE_INST(13, 1) WG_WAVE_INST(15, 1) WG_WAVE_INST(15, 4)
 template __global__ void k_lean<WG_MODE_SEAL>(StreamParams);
 template __global__ void k_lean<WG_MODE_OPEN>(StreamParams);
 template __global__ void k_pipe<WG_MODE_SEAL, 0>(StreamParams);
