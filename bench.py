@@ -215,6 +215,7 @@ def main():
     ap.add_argument("--workload", default="c1", choices=["c1", "c2", "c3", "c4"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-mem", default="pinned", choices=["pinned", "pageable"])
+    ap.add_argument("--streams", type=int, default=1)
     args = ap.parse_args()
     if args.workload == "c4":
         return host_bench(args)
@@ -252,12 +253,36 @@ def main():
     status = torch.zeros(n, dtype=torch.int32, device=dev)
     max_len = int(lengths.max())
 
-    def step():
-        eng.seal(d_desc, pt, ct, max_len, uniform=uniform)
-        eng.open(d_desc, ct, back, status, max_len, uniform=uniform)
+    # --streams K: the batch is cut into K runs of consecutive packets, each sealed and
+    # then opened on its own stream; the runs' kernels overlap, so one run's launch tail
+    # is filled by another run's waves (the work and every packet's seal -> open order
+    # are unchanged)
+    K = max(1, args.streams)
+    cuts = [n * i // K for i in range(K + 1)]
+    main_stream = torch.cuda.current_stream()
+    side = [main_stream] if K == 1 else [torch.cuda.Stream(device=dev) for _ in range(K)]
 
+    def step():
+        for i in range(K):
+            a, b = cuts[i], cuts[i + 1]
+            with torch.cuda.stream(side[i]):
+                eng.seal(d_desc[a:b], pt, ct, max_len, uniform=uniform)
+                eng.open(d_desc[a:b], ct, back, status[a:b], max_len, uniform=uniform)
+
+    def fork():
+        if K > 1:
+            for s_ in side:
+                s_.wait_stream(main_stream)
+
+    def join():
+        if K > 1:
+            for s_ in side:
+                main_stream.wait_stream(s_)
+
+    fork()
     for _ in range(args.warmup):
         step()
+    join()
     torch.cuda.synchronize()
 
     # HIP events on the stream the kernels are launched on (torch's current stream,

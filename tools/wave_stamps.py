@@ -9,6 +9,7 @@ import sys
 import numpy as np
 import torch
 
+torch.cuda.is_available()  # torch's HIP runtime first (tests/conftest.py)
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 wg = importlib.import_module("wireguard-java_amd")
 E = importlib.import_module("wireguard-java_amd.engine")

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "wg_kernels.hip"
+#include "wg_lane.h"
 
 namespace {
 
@@ -119,8 +120,12 @@ struct Tunables {
   int use_lean = 0;                                         // k_lean (state in LDS) for transport
   uint32_t stream_lds_pad = 0;                              // dynamic LDS per wave: caps occupancy
   int use_wave = 1;                                         // k_wave (8 waves/SIMD layout): the default
-  int wave_variant = 5;                                     // k_wave<MODE, V, WPG>: prefetch + progress priority
+  int wave_variant = 5;                                     // k_wave<SEAL, V, WPG>: prefetch + progress priority
+  int wave_variant_open = 5;                                // k_wave<OPEN, V, WPG>
   int wave_wpg = 1;                                         // k_wave waves per workgroup (1, 4, 8)
+  int use_lane = 0;                                         // k_lane (K lanes per packet, contiguous block ranges)
+  int lane_k = 2;                                           // k_lane lanes per packet (1, 2, 4, 8)
+  int lane_variant = 1;                                     // k_lane<MODE, K, V> variant bits
   Tunables() {
     if (const char* e = getenv("WG_STREAM_LDS_PAD")) stream_lds_pad = (uint32_t)std::min(65536, std::max(0, atoi(e)));
     if (const char* e = getenv("WG_STREAM_PPW")) stream_ppw_uniform = stream_ppw_mixed = std::max(1, atoi(e));
@@ -130,9 +135,19 @@ struct Tunables {
       use_pipe = strcmp(e, "pipe") == 0;
       use_lean = strcmp(e, "lean") == 0;
       use_wave = strcmp(e, "wave") == 0 || strcmp(e, "default") == 0;
+      use_lane = strcmp(e, "lane") == 0;
     }
-    if (const char* e = getenv("WG_WAVE_VARIANT")) wave_variant = atoi(e) & 15;
-    if (const char* e = getenv("WG_WAVE_WPG")) wave_wpg = atoi(e) == 4 ? 4 : atoi(e) == 8 ? 8 : 1;
+    if (const char* e = getenv("WG_WAVE_VARIANT")) wave_variant = wave_variant_open = atoi(e) & 127;
+    if (const char* e = getenv("WG_WAVE_VARIANT_OPEN")) wave_variant_open = atoi(e) & 127;
+    if (const char* e = getenv("WG_WAVE_WPG")) {
+      const int g = atoi(e);
+      wave_wpg = (g == 4 || g == 8 || g == 16) ? g : 1;
+    }
+    if (const char* e = getenv("WG_LANE_K")) {
+      const int k = atoi(e);
+      lane_k = (k == 1 || k == 2 || k == 4 || k == 8) ? k : 2;
+    }
+    if (const char* e = getenv("WG_LANE_VARIANT")) lane_variant = atoi(e) & 3;
     if (const char* e = getenv("WG_STREAM_VARIANT")) stream_variant = atoi(e) & 127;
     if (const char* e = getenv("WG_TILE_PASSES")) tile_passes = std::min(4u, std::max(1u, (uint32_t)atoi(e)));
     if (const char* e = getenv("WG_POLY_WAVES")) poly_waves = std::min(4u, std::max(1u, (uint32_t)atoi(e)));
@@ -268,6 +283,38 @@ int launch_tiles(wg_ctx* c, const void* desc, uint32_t n, const uint8_t* in, uin
   return WG_OK;
 }
 
+// k_wave<MODE, V, G> for the variant bits V (see wg_kernels.hip) and G waves per workgroup
+template <int MODE, int G>
+void launch_wave(int V, uint32_t wgrid, hipStream_t s, const wgk::StreamParams& P) {
+  switch (V) {
+#define WG_WV(VV) \
+  case VV: hipLaunchKernelGGL((wgk::k_wave<MODE, VV, G>), dim3(wgrid), dim3(64 * G), 0, s, P); break;
+    WG_WV(0) WG_WV(1) WG_WV(3) WG_WV(7) WG_WV(13) WG_WV(15) WG_WV(65) WG_WV(67) WG_WV(69) WG_WV(71)
+#undef WG_WV
+    default: hipLaunchKernelGGL((wgk::k_wave<MODE, 5, G>), dim3(wgrid), dim3(64 * G), 0, s, P); break;
+  }
+}
+
+// k_lane<MODE, K, V>: K lanes per packet, 256-thread workgroups
+template <int MODE, int K>
+void launch_lane_k(int V, uint32_t n, hipStream_t s, const wgk::StreamParams& P) {
+  const uint32_t grid = (uint32_t)(((uint64_t)n * K + 255u) / 256u);
+  switch (V) {
+    case 0: hipLaunchKernelGGL((wgk::k_lane<MODE, K, 0>), dim3(grid), dim3(256), 0, s, P); break;
+    case 3: hipLaunchKernelGGL((wgk::k_lane<MODE, K, 3>), dim3(grid), dim3(256), 0, s, P); break;
+    default: hipLaunchKernelGGL((wgk::k_lane<MODE, K, 1>), dim3(grid), dim3(256), 0, s, P); break;
+  }
+}
+template <int MODE>
+void launch_lane(int K, int V, uint32_t n, hipStream_t s, const wgk::StreamParams& P) {
+  switch (K) {
+    case 1: launch_lane_k<MODE, 1>(V, n, s, P); break;
+    case 4: launch_lane_k<MODE, 4>(V, n, s, P); break;
+    case 8: launch_lane_k<MODE, 8>(V, n, s, P); break;
+    default: launch_lane_k<MODE, 2>(V, n, s, P); break;
+  }
+}
+
 // the caller's stream as-is: NULL is HIP's default (null) stream, like every HIP API;
 // pass wg_ctx_stream(ctx) to use the context's own non-blocking stream
 // Transport seal/open through k_stream (one wave per workgroup, 8 packet slots).
@@ -297,27 +344,18 @@ int launch_stream(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
   const uint32_t pad = tunables().stream_lds_pad;
   hipEvent_t ev;
   record_start(c, s, &ev);
-  if (tunables().use_wave) {
-    const int G = tunables().wave_wpg, V = tunables().wave_variant;
+  if (tunables().use_lane) {
+    launch_lane<MODE>(tunables().lane_k, tunables().lane_variant, n, s, P);
+  } else if (tunables().use_wave) {
+    const int G = tunables().wave_wpg;
+    const int V = MODE == WG_MODE_OPEN ? tunables().wave_variant_open : tunables().wave_variant;
     const uint32_t wgrid = (grid + G - 1) / G;
-#define WG_WAVE_LAUNCH(VV, GG) hipLaunchKernelGGL((wgk::k_wave<MODE, VV, GG>), dim3(wgrid), dim3(64 * GG), 0, s, P)
-    if (G == 1) {
-      switch (V) {
-        case 0: WG_WAVE_LAUNCH(0, 1); break;
-        case 1: WG_WAVE_LAUNCH(1, 1); break;
-        case 2: WG_WAVE_LAUNCH(2, 1); break;
-        case 5: WG_WAVE_LAUNCH(5, 1); break;
-        case 7: WG_WAVE_LAUNCH(7, 1); break;
-        case 13: WG_WAVE_LAUNCH(13, 1); break;
-        case 15: WG_WAVE_LAUNCH(15, 1); break;
-        default: WG_WAVE_LAUNCH(3, 1); break;
-      }
-    } else if (G == 4) {
-      if (V == 15) WG_WAVE_LAUNCH(15, 4); else if (V & 2) WG_WAVE_LAUNCH(3, 4); else WG_WAVE_LAUNCH(1, 4);
-    } else {
-      if (V & 2) WG_WAVE_LAUNCH(3, 8); else WG_WAVE_LAUNCH(1, 8);
+    switch (G) {
+      case 4: launch_wave<MODE, 4>(V, wgrid, s, P); break;
+      case 8: launch_wave<MODE, 8>(V, wgrid, s, P); break;
+      case 16: launch_wave<MODE, 16>(V, wgrid, s, P); break;
+      default: launch_wave<MODE, 1>(V, wgrid, s, P); break;
     }
-#undef WG_WAVE_LAUNCH
   } else if (tunables().use_lean) {
     hipLaunchKernelGGL((wgk::k_lean<MODE>), dim3(grid), dim3(64), 0, s, P);
   } else if (tunables().use_pipe) {

@@ -46,9 +46,28 @@ __device__ __forceinline__ void chacha20_block(const uint32_t k[8], uint32_t ctr
   out[8] = x8 + k[4]; out[9] = x9 + k[5]; out[10] = x10 + k[6]; out[11] = x11 + k[7];
   out[12] = x12 + ctr; out[13] = x13 + n0; out[14] = x14 + n1; out[15] = x15 + n2;
 }
+// rotl16(d ^ a) as two SDWA xors, one per 16-bit half (the halves swap places):
+// VOP2-SDWA issue instead of v_xor_b32 + v_perm_b32 (tools/microbench6.hip).
+__device__ __forceinline__ uint32_t xor_rotl16_sdwa(uint32_t d, uint32_t a) {
+  uint32_t t;
+  asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0"
+      : "=&v"(t) : "v"(d), "v"(a));
+  asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1"
+      : "+v"(t) : "v"(d), "v"(a));
+  return t;
+}
+
+#define WG_QR_SDWA(a, b, c, d)             \
+  a += b; d = xor_rotl16_sdwa(d, a);       \
+  c += d; b ^= c; b = rotl(b, 12);         \
+  a += b; d ^= a; d = rotl8(d);            \
+  c += d; b ^= c; b = rotl(b, 7);
+
 // Same block, key read from LDS twice (before the rounds and again for the
 // feed-forward) so the 8 key words are not live across the 20 rounds; the
 // "memory" clobber keeps the compiler from merging the two reads.
+// SDWA: rotl16 as two SDWA xors instead of v_xor + v_perm.
+template <bool SDWA = false>
 __device__ __forceinline__ void chacha20_block_lds(const uint4* key_lds, uint32_t ctr, uint32_t n0, uint32_t n1,
                                                    uint32_t n2, uint32_t out[16]) {
   uint4 ka = key_lds[0], kb = key_lds[1];
@@ -57,8 +76,13 @@ __device__ __forceinline__ void chacha20_block_lds(const uint4* key_lds, uint32_
   uint32_t x12 = ctr, x13 = n0, x14 = n1, x15 = n2;
 #pragma unroll 2
   for (int r = 0; r < 10; ++r) {
-    WG_QR(x0, x4, x8, x12) WG_QR(x1, x5, x9, x13) WG_QR(x2, x6, x10, x14) WG_QR(x3, x7, x11, x15)
-    WG_QR(x0, x5, x10, x15) WG_QR(x1, x6, x11, x12) WG_QR(x2, x7, x8, x13) WG_QR(x3, x4, x9, x14)
+    if constexpr (SDWA) {
+      WG_QR_SDWA(x0, x4, x8, x12) WG_QR_SDWA(x1, x5, x9, x13) WG_QR_SDWA(x2, x6, x10, x14) WG_QR_SDWA(x3, x7, x11, x15)
+      WG_QR_SDWA(x0, x5, x10, x15) WG_QR_SDWA(x1, x6, x11, x12) WG_QR_SDWA(x2, x7, x8, x13) WG_QR_SDWA(x3, x4, x9, x14)
+    } else {
+      WG_QR(x0, x4, x8, x12) WG_QR(x1, x5, x9, x13) WG_QR(x2, x6, x10, x14) WG_QR(x3, x7, x11, x15)
+      WG_QR(x0, x5, x10, x15) WG_QR(x1, x6, x11, x12) WG_QR(x2, x7, x8, x13) WG_QR(x3, x4, x9, x14)
+    }
   }
   asm volatile("" ::: "memory");
   ka = key_lds[0];
@@ -69,6 +93,7 @@ __device__ __forceinline__ void chacha20_block_lds(const uint4* key_lds, uint32_
   out[12] = x12 + ctr; out[13] = x13 + n0; out[14] = x14 + n1; out[15] = x15 + n2;
 }
 #undef WG_QR
+#undef WG_QR_SDWA
 
 // ---- Poly1305, radix 2^26 -------------------------------------------------
 // An element of Z/(2^130-5) as 5 limbs h[i] (value = sum h[i] 2^(26 i)), kept

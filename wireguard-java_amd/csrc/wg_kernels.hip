@@ -1346,6 +1346,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8))) k_
 //    block barriers): one-wave workgroups are dispatched at only ~1 per 11 cycles
 //    chip-wide, which left a 65536-packet launch with ~40% of its wave slots empty.
 // Results are identical to k_stream (same Horner order, same finish).
+// Variant bits V: 1 prefetch the round's payload before the ChaCha rounds,
+// 2 amdgpu_waves_per_eu(8) (cap at 64 VGPRs), 4 progress-based s_setprio,
+// 8 every lane reads the descriptor (round-0 payload requested with it),
+// 16 rotl16 as SDWA xors (wg_device.h xor_rotl16_sdwa; measured no faster),
+// 32 slot keys through scalar loads (fetch_slot_keys; measured no faster),
+// 64 workgroup-lockstep rounds (one barrier per round).
 __device__ __forceinline__ uint32_t opaque_lane() {
   uint32_t x = threadIdx.x & 63u;
   asm volatile("" : "+v"(x));
@@ -1353,6 +1359,35 @@ __device__ __forceinline__ uint32_t opaque_lane() {
 }
 // orders this wave's LDS writes before its other lanes' reads (LDS is in order per wave)
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Scalar loads of the keys of the slots whose bit 8s is set in `need` (lane 8s holds
+// the slot's key index in `key_slot`), two slots per statement, written to skey.
+// The loads and their wait sit in one asm statement (cdna_hip_programming.md §5.7).
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void fetch_slot_keys(const uint32_t* keys, uint32_t key_slot, unsigned long long need,
+                                                uint4* skey) {
+  const uint32_t lane = opaque_lane();
+#pragma unroll
+  for (int ss = 0; ss < 8; ss += 2) {
+    const bool na = (need >> (8 * ss)) & 1ull, nb = (need >> (8 * ss + 8)) & 1ull;
+    if (!na && !nb) continue;  // wave-uniform
+    const uint32_t ka = __builtin_amdgcn_readlane(key_slot, 8 * ss);
+    const uint32_t kb = __builtin_amdgcn_readlane(key_slot, 8 * ss + 8);
+    const uint32_t* pa = keys + 8u * (na ? ka : 0u);
+    const uint32_t* pb = keys + 8u * (nb ? kb : 0u);
+    u32x8 a, b;
+    asm volatile("s_load_dwordx8 %0, %2, 0x0\n\ts_load_dwordx8 %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(a), "=&s"(b) : "s"(pa), "s"(pb));
+    if (na && lane == 8u * ss) {
+      skey[2 * ss] = make_uint4(a[0], a[1], a[2], a[3]);
+      skey[2 * ss + 1] = make_uint4(a[4], a[5], a[6], a[7]);
+    }
+    if (nb && lane == 8u * ss + 8u) {
+      skey[2 * ss + 2] = make_uint4(b[0], b[1], b[2], b[3]);
+      skey[2 * ss + 3] = make_uint4(b[4], b[5], b[6], b[7]);
+    }
+  }
+}
 
 template <int MODE, int V, int WPG>
 __global__ void __launch_bounds__(64 * WPG) __attribute__((amdgpu_waves_per_eu((V & 2) ? 8 : 1)))
@@ -1375,10 +1410,14 @@ k_wave(StreamParams P) {
   bool have = pkt < w1;
   uint32_t round = 0;
   uint32_t acc[5], W[5];
+  uint32_t key_slot = ~0u;  // V & 32: lane 0 of a starting slot holds its key slot
   WG_PH_DECL
   uint32_t wave_rounds = 0;  // wave-uniform
 
-  while (__any(have)) {
+  // V & 64: the workgroup's waves advance round by round together (one barrier per
+  // round; every wave runs the same trip count, idle once its slots are done), so a
+  // workgroup's waves finish together instead of trickling out of the SIMDs.
+  while ((V & 64) ? (__syncthreads_or(have ? 1 : 0) != 0) : __any(have)) {
     if constexpr ((V & 4) != 0) progress_prio(wave_rounds++);
     WG_PH_MARK();
     uint32_t w[16];
@@ -1403,7 +1442,9 @@ k_wave(StreamParams P) {
         if (j == 0) {
           srec[2 * s] = lo;
           srec[2 * s + 1] = make_uint4(hi.x, hi.y, len, valid ? 1u : 0u);
-          if (valid) {
+          if constexpr ((V & 32) != 0) {
+            if (valid) key_slot = ks_;
+          } else if (valid) {
             const uint4* kp = (const uint4*)(P.keys + 8u * ks_);
             skey[2 * s] = kp[0];
             skey[2 * s + 1] = kp[1];
@@ -1412,6 +1453,14 @@ k_wave(StreamParams P) {
       }
 #pragma unroll
       for (int i = 0; i < 5; ++i) acc[i] = 0;
+    }
+    if constexpr ((V & 32) != 0) {
+      // the starting slots' keys through the scalar cache: one L2 request per SQC
+      // instead of one per wave, so a key shared by many packets (one session)
+      // does not serialise every wave of the launch on one L2 channel
+      const unsigned long long need = __ballot(key_slot != ~0u);  // bit 8s: slot s starts a valid packet
+      if (need) fetch_slot_keys(P.keys, key_slot, need, skey);
+      key_slot = ~0u;
     }
     wave_lds_sync();  // the record writes before the slot's other lanes read them
     WG_PH_ADD(0);
@@ -1434,7 +1483,7 @@ k_wave(StreamParams P) {
       }
       if (act) {
         uint32_t ks[16];
-        chacha20_block_lds(&skey[2 * s], b, rc.x, rc.y, 0u, ks);
+        chacha20_block_lds<(V & 16) != 0>(&skey[2 * s], b, rc.x, rc.y, 0u, ks);
         if (!data) {
           sotk[2 * s] = make_uint4(ks[0], ks[1], ks[2], ks[3]);
           sotk[2 * s + 1] = make_uint4(ks[4], ks[5], ks[6], ks[7]);
@@ -1601,12 +1650,6 @@ WG_STREAM_INST(0) WG_STREAM_INST(1) WG_STREAM_INST(2) WG_STREAM_INST(3)
 WG_STREAM_INST(4) WG_STREAM_INST(5) WG_STREAM_INST(6) WG_STREAM_INST(7)
 WG_STREAM_INST(9) WG_STREAM_INST(11) WG_STREAM_INST(15) WG_STREAM_INST(17) WG_STREAM_INST(33) WG_STREAM_INST(49)
 WG_STREAM_INST(65) WG_STREAM_INST(73)
-#define WG_WAVE_INST(V, G)                                                \
-  template __global__ void k_wave<WG_MODE_SEAL, V, G>(StreamParams); \
-  template __global__ void k_wave<WG_MODE_OPEN, V, G>(StreamParams);
-WG_WAVE_INST(0, 1) WG_WAVE_INST(1, 1) WG_WAVE_INST(2, 1) WG_WAVE_INST(3, 1)
-WG_WAVE_INST(1, 4) WG_WAVE_INST(3, 4) WG_WAVE_INST(1, 8) WG_WAVE_INST(3, 8)
-WG_WAVE_INST(5, 1) WG_WAVE_INST(7, 1) WG_WAVE_INST(13, 1) WG_WAVE_INST(15, 1) WG_WAVE_INST(15, 4)
 template __global__ void k_lean<WG_MODE_SEAL>(StreamParams);
 template __global__ void k_lean<WG_MODE_OPEN>(StreamParams);
 template __global__ void k_pipe<WG_MODE_SEAL, 0>(StreamParams);
