@@ -77,6 +77,7 @@ struct wg_ctx {
   uint32_t* keys = nullptr;  // device key table
   // non-uniform plan workspace
   DevBuf plan_nb, plan_prefix, plan_tiles, plan_ntiles, plan_tmp;
+  DevBuf sink;  // k_coop scratch
   // host-API staging
   DevBuf h_desc, h_in, h_out, h_aad, h_status, h_keys;
   std::mutex mu;  // serialises host-API calls and plan workspace reuse
@@ -125,7 +126,10 @@ struct Tunables {
   int wave_wpg = 1;                                         // k_wave waves per workgroup (1, 4, 8)
   int use_lane = 0;                                         // k_lane (K lanes per packet, contiguous block ranges)
   int lane_k = 2;                                           // k_lane lanes per packet (1, 2, 4, 8)
-  int lane_variant = 1;                                     // k_lane<MODE, K, V> variant bits
+  int use_coop = 0;                                         // k_coop (k_lane ranges + cooperative coalesced IO)
+  int use_quad = 0;                                         // k_quad (k_lane K=4 with quad-cooperative IO)
+  int quad_variant = 0;                                     // k_quad<MODE, V> variant bits
+  int lane_variant = 5;                                     // k_lane<MODE, K, V> variant bits
   Tunables() {
     if (const char* e = getenv("WG_STREAM_LDS_PAD")) stream_lds_pad = (uint32_t)std::min(65536, std::max(0, atoi(e)));
     if (const char* e = getenv("WG_STREAM_PPW")) stream_ppw_uniform = stream_ppw_mixed = std::max(1, atoi(e));
@@ -136,9 +140,11 @@ struct Tunables {
       use_lean = strcmp(e, "lean") == 0;
       use_wave = strcmp(e, "wave") == 0 || strcmp(e, "default") == 0;
       use_lane = strcmp(e, "lane") == 0;
+      use_quad = strcmp(e, "quad") == 0;
+      use_coop = strcmp(e, "coop") == 0;
     }
-    if (const char* e = getenv("WG_WAVE_VARIANT")) wave_variant = wave_variant_open = atoi(e) & 127;
-    if (const char* e = getenv("WG_WAVE_VARIANT_OPEN")) wave_variant_open = atoi(e) & 127;
+    if (const char* e = getenv("WG_WAVE_VARIANT")) wave_variant = wave_variant_open = atoi(e) & 255;
+    if (const char* e = getenv("WG_WAVE_VARIANT_OPEN")) wave_variant_open = atoi(e) & 255;
     if (const char* e = getenv("WG_WAVE_WPG")) {
       const int g = atoi(e);
       wave_wpg = (g == 4 || g == 8 || g == 16) ? g : 1;
@@ -147,7 +153,8 @@ struct Tunables {
       const int k = atoi(e);
       lane_k = (k == 1 || k == 2 || k == 4 || k == 8) ? k : 2;
     }
-    if (const char* e = getenv("WG_LANE_VARIANT")) lane_variant = atoi(e) & 3;
+    if (const char* e = getenv("WG_LANE_VARIANT")) lane_variant = atoi(e) & 63;
+    if (const char* e = getenv("WG_QUAD_VARIANT")) quad_variant = atoi(e) & 63;
     if (const char* e = getenv("WG_STREAM_VARIANT")) stream_variant = atoi(e) & 127;
     if (const char* e = getenv("WG_TILE_PASSES")) tile_passes = std::min(4u, std::max(1u, (uint32_t)atoi(e)));
     if (const char* e = getenv("WG_POLY_WAVES")) poly_waves = std::min(4u, std::max(1u, (uint32_t)atoi(e)));
@@ -290,6 +297,7 @@ void launch_wave(int V, uint32_t wgrid, hipStream_t s, const wgk::StreamParams& 
 #define WG_WV(VV) \
   case VV: hipLaunchKernelGGL((wgk::k_wave<MODE, VV, G>), dim3(wgrid), dim3(64 * G), 0, s, P); break;
     WG_WV(0) WG_WV(1) WG_WV(3) WG_WV(7) WG_WV(13) WG_WV(15) WG_WV(65) WG_WV(67) WG_WV(69) WG_WV(71)
+    WG_WV(132) WG_WV(133) WG_WV(134) WG_WV(135)
 #undef WG_WV
     default: hipLaunchKernelGGL((wgk::k_wave<MODE, 5, G>), dim3(wgrid), dim3(64 * G), 0, s, P); break;
   }
@@ -298,11 +306,28 @@ void launch_wave(int V, uint32_t wgrid, hipStream_t s, const wgk::StreamParams& 
 // k_lane<MODE, K, V>: K lanes per packet, 256-thread workgroups
 template <int MODE, int K>
 void launch_lane_k(int V, uint32_t n, hipStream_t s, const wgk::StreamParams& P) {
-  const uint32_t grid = (uint32_t)(((uint64_t)n * K + 255u) / 256u);
   switch (V) {
-    case 0: hipLaunchKernelGGL((wgk::k_lane<MODE, K, 0>), dim3(grid), dim3(256), 0, s, P); break;
-    case 3: hipLaunchKernelGGL((wgk::k_lane<MODE, K, 3>), dim3(grid), dim3(256), 0, s, P); break;
-    default: hipLaunchKernelGGL((wgk::k_lane<MODE, K, 1>), dim3(grid), dim3(256), 0, s, P); break;
+#define WG_LV(VV)                                                                                        \
+  case VV: {                                                                                             \
+    constexpr uint32_t T = wgk::lane_wg_threads<VV>();                                                  \
+    const uint32_t grid = (uint32_t)(((uint64_t)n * K + T - 1u) / T);                                   \
+    hipLaunchKernelGGL((wgk::k_lane<MODE, K, VV>), dim3(grid), dim3(T), 0, s, P);                        \
+  } break;
+    WG_LV(1) WG_LV(3) WG_LV(7)
+#undef WG_LV
+#define WG_LA(VV)                                                                                        \
+  case VV:                                                                                               \
+    if constexpr (K == 2) {                                                                              \
+      const uint32_t grid = (uint32_t)(((uint64_t)n * K + 63u) / 64u);                                   \
+      hipLaunchKernelGGL((wgk::k_lane<MODE, K, VV>), dim3(grid), dim3(64), 0, s, P);                     \
+    }                                                                                                    \
+    break;
+    WG_LA(13) WG_LA(21) WG_LA(29) WG_LA(53)
+#undef WG_LA
+    default: {
+      const uint32_t grid = (uint32_t)(((uint64_t)n * K + 63u) / 64u);
+      hipLaunchKernelGGL((wgk::k_lane<MODE, K, 5>), dim3(grid), dim3(64), 0, s, P);
+    } break;
   }
 }
 template <int MODE>
@@ -340,11 +365,34 @@ int launch_stream(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
 #ifdef WG_DIAG
   P.stamps = g_stamps;
 #endif
+  if (tunables().use_coop) {
+    int rc;
+    if ((rc = c->sink.ensure(wgk::kCoopSinkBytes)) != WG_OK) return rc;
+    P.sink = (uint8_t*)c->sink.p;
+  }
   const uint32_t grid = (n + P.ppw - 1) / P.ppw;
   const uint32_t pad = tunables().stream_lds_pad;
   hipEvent_t ev;
   record_start(c, s, &ev);
-  if (tunables().use_lane) {
+  if (tunables().use_coop) {
+    const uint32_t K = tunables().lane_k == 1 ? 1u : (tunables().lane_k == 4 ? 4u : 2u);
+    const uint32_t cgrid = (uint32_t)(((uint64_t)n * K + 63u) / 64u);
+    const int CV = tunables().lane_variant;
+    if (K == 2 && CV == 8) hipLaunchKernelGGL((wgk::k_coop<MODE, 2, 8>), dim3(cgrid), dim3(64), 0, s, P);
+    else if (K == 2 && CV == 48) hipLaunchKernelGGL((wgk::k_coop<MODE, 2, 48>), dim3(cgrid), dim3(64), 0, s, P);
+    else if (K == 2 && CV == 16) hipLaunchKernelGGL((wgk::k_coop<MODE, 2, 16>), dim3(cgrid), dim3(64), 0, s, P);
+    else if (K == 1) hipLaunchKernelGGL((wgk::k_coop<MODE, 1, 0>), dim3(cgrid), dim3(64), 0, s, P);
+    else if (K == 4) hipLaunchKernelGGL((wgk::k_coop<MODE, 4, 0>), dim3(cgrid), dim3(64), 0, s, P);
+    else hipLaunchKernelGGL((wgk::k_coop<MODE, 2, 0>), dim3(cgrid), dim3(64), 0, s, P);
+  } else if (tunables().use_quad) {
+    const uint32_t qgrid = (uint32_t)(((uint64_t)n * 4u + 63u) / 64u);
+    switch (tunables().quad_variant) {
+      case 2: hipLaunchKernelGGL((wgk::k_quad<MODE, 2>), dim3(qgrid), dim3(64), 0, s, P); break;
+      case 16: hipLaunchKernelGGL((wgk::k_quad<MODE, 16>), dim3(qgrid), dim3(64), 0, s, P); break;
+      case 48: hipLaunchKernelGGL((wgk::k_quad<MODE, 48>), dim3(qgrid), dim3(64), 0, s, P); break;
+      default: hipLaunchKernelGGL((wgk::k_quad<MODE, 0>), dim3(qgrid), dim3(64), 0, s, P); break;
+    }
+  } else if (tunables().use_lane) {
     launch_lane<MODE>(tunables().lane_k, tunables().lane_variant, n, s, P);
   } else if (tunables().use_wave) {
     const int G = tunables().wave_wpg;
@@ -438,7 +486,7 @@ int wg_ctx_destroy(wg_ctx* c) {
     (void)hipEventDestroy(e.second);
   }
   for (DevBuf* b : {&c->plan_nb, &c->plan_prefix, &c->plan_tiles, &c->plan_ntiles, &c->plan_tmp, &c->h_desc, &c->h_in,
-                    &c->h_out, &c->h_aad, &c->h_status, &c->h_keys})
+                    &c->h_out, &c->h_aad, &c->h_status, &c->h_keys, &c->sink})
     b->release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
