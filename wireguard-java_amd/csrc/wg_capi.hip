@@ -126,6 +126,7 @@ struct Tunables {
   int wave_wpg = 1;                                         // k_wave waves per workgroup (1, 4, 8)
   int use_lane = 0;                                         // k_lane (K lanes per packet, contiguous block ranges)
   int lane_k = 2;                                           // k_lane lanes per packet (1, 2, 4, 8)
+  int use_ws = 0;                                           // k_ws (warp-specialised producer/consumer waves)
   int use_coop = 0;                                         // k_coop (k_lane ranges + cooperative coalesced IO)
   int use_quad = 0;                                         // k_quad (k_lane K=4 with quad-cooperative IO)
   int quad_variant = 0;                                     // k_quad<MODE, V> variant bits
@@ -142,6 +143,7 @@ struct Tunables {
       use_lane = strcmp(e, "lane") == 0;
       use_quad = strcmp(e, "quad") == 0;
       use_coop = strcmp(e, "coop") == 0;
+      use_ws = strcmp(e, "ws") == 0;
     }
     if (const char* e = getenv("WG_WAVE_VARIANT")) wave_variant = wave_variant_open = atoi(e) & 255;
     if (const char* e = getenv("WG_WAVE_VARIANT_OPEN")) wave_variant_open = atoi(e) & 255;
@@ -374,7 +376,15 @@ int launch_stream(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
   const uint32_t pad = tunables().stream_lds_pad;
   hipEvent_t ev;
   record_start(c, s, &ev);
-  if (tunables().use_coop) {
+  if (tunables().use_ws && (flags & WG_F_UNIFORM)) {
+    const uint32_t K = tunables().lane_k == 1 ? 1u : (tunables().lane_k == 4 ? 4u : 2u);
+    const uint32_t wgrid = (uint32_t)(((uint64_t)n * K + 511u) / 512u);
+    if (K == 1) hipLaunchKernelGGL((wgk::k_ws<MODE, 1>), dim3(wgrid), dim3(640), 0, s, P);
+    else if (K == 4) hipLaunchKernelGGL((wgk::k_ws<MODE, 4>), dim3(wgrid), dim3(640), 0, s, P);
+    else hipLaunchKernelGGL((wgk::k_ws<MODE, 2>), dim3(wgrid), dim3(640), 0, s, P);
+    if (MODE == WG_MODE_OPEN && status)
+      hipLaunchKernelGGL(wgk::k_ws_scrub, dim3((uint32_t)(((uint64_t)n * 16u + 255u) / 256u)), dim3(256), 0, s, P);
+  } else if (tunables().use_coop) {
     const uint32_t K = tunables().lane_k == 1 ? 1u : (tunables().lane_k == 4 ? 4u : 2u);
     const uint32_t cgrid = (uint32_t)(((uint64_t)n * K + 63u) / 64u);
     const int CV = tunables().lane_variant;

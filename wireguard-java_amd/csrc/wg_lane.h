@@ -871,4 +871,320 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_ws — warp-specialised transport kernel: k_lane's contiguous block ranges computed
+// by 8 consumer waves out of LDS while 2 producer waves move the payload between HBM
+// and LDS, so the ARX rounds and the payload stream run at the same time instead of
+// taking turns inside every wave. One workgroup = 10 waves; the
+// 512 consumer lanes own 512/K packets (K lanes each). Round t of every consumer lane
+// lives in LDS row `lane` of buffer t % 2 (64 B; chunk c at 16 * ((c + row/4) & 3) so
+// a wave's row reads spread over the banks). Stage t, between two workgroup barriers:
+//   consumers: read their row, keystream + XOR, write the output block back into it,
+//              Poly1305 from registers;
+//   producers: store stage t-1's output rows (ds_read -> global_store), then load
+//              stage t+1's rows into the same buffer with global_load_lds_dwordx4
+//              (16 rows of 64 contiguous bytes per wave instruction), then wait.
+// Partial chunks (packet tails) and unaligned packets take byte-wise paths in the
+// producer. The round count T is uniform over the launch (from max_len), so every
+// wave passes the same barriers; this kernel serves uniform batches.
+struct WsPkt {  // per-packet record in LDS, written by the packet's first consumer lane
+  uint32_t in_lo, in_hi, out_lo, out_hi;
+  uint32_t len, flags, q, nb;  // flags: 1 valid, 2 in/out 16-B aligned
+};
+
+template <int MODE, int K>
+__global__ void __launch_bounds__(640) k_ws(StreamParams P) {
+  static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
+  static_assert(K == 1 || K == 2 || K == 4, "lanes per packet");
+  constexpr uint32_t NC = 512, NPK = NC / K;  // consumer lanes, packets per workgroup
+  __shared__ uint4 rows[2][NC * 4];           // 2 x 32 KB
+  __shared__ WsPkt tab[NPK];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool consumer = wave < 8u;
+  const uint32_t nbmax = ((P.max_len + 63u) >> 6) + 1u;
+  const uint32_t T = (nbmax + K - 1u) / K;  // rounds, uniform over the launch
+  auto rowpos = [](uint32_t row, uint32_t c) -> uint32_t { return 4u * row + ((c + (row >> 2)) & 3u); };
+
+  // ---- consumer state ----
+  const uint32_t lane = tid;  // consumer lane = row
+  const uint64_t gid = (uint64_t)blockIdx.x * NC + lane;
+  const uint32_t pkt = (uint32_t)(gid / K), h = (uint32_t)(gid % K);
+  bool valid = false;
+  uint32_t len = 0, ctr_lo = 0, ctr_hi = 0, nb = 1, Q = 1, b0 = 0, nr = 0;
+  uint64_t in_off = 0, out_off = 0;
+  uint32_t key[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (consumer) {
+    const bool in_grid = gid < (uint64_t)P.n * K;
+    uint4 lo = make_uint4(0, 0, 0, 0), hi = make_uint4(0, 0, 0, 0);
+    if (in_grid) {
+      const uint4* dp = (const uint4*)(P.desc + pkt);
+      lo = dp[0];
+      hi = dp[1];
+    }
+    in_off = (uint64_t)lo.x | ((uint64_t)lo.y << 32);
+    out_off = (uint64_t)lo.z | ((uint64_t)lo.w << 32);
+    ctr_lo = hi.x; ctr_hi = hi.y; len = hi.z;
+    const uint32_t kslot = hi.w;
+    valid = in_grid && len <= P.max_len && kslot < P.key_slots;
+    const uint64_t in_need = (uint64_t)len + (MODE == WG_MODE_OPEN ? 16u : 0u);
+    const uint64_t out_need = (uint64_t)len + (MODE == WG_MODE_SEAL ? 16u : 0u);
+    valid = valid && in_off <= P.in_size && in_need <= P.in_size - in_off;
+    valid = valid && out_off <= P.out_size && out_need <= P.out_size - out_off;
+    nb = ((len + 63u) >> 6) + 1u;
+    Q = (nb + K - 1u) / K;
+    b0 = h * Q;
+    nr = (valid && b0 < nb) ? min(Q, nb - b0) : 0u;
+    if (valid) {
+      const uint4* kp = (const uint4*)(P.keys + 8u * kslot);
+      const uint4 ka = kp[0], kb = kp[1];
+      key[0] = ka.x; key[1] = ka.y; key[2] = ka.z; key[3] = ka.w;
+      key[4] = kb.x; key[5] = kb.y; key[6] = kb.z; key[7] = kb.w;
+    }
+    if (h == 0) {
+      const uint64_t ia = (uint64_t)(uintptr_t)(P.in + in_off), oa = (uint64_t)(uintptr_t)(P.out + out_off);
+      WsPkt r;
+      r.in_lo = (uint32_t)ia; r.in_hi = (uint32_t)(ia >> 32);
+      r.out_lo = (uint32_t)oa; r.out_hi = (uint32_t)(oa >> 32);
+      r.len = len;
+      r.flags = (valid ? 1u : 0u) | ((((ia | oa) & 15u) == 0) ? 2u : 0u);
+      r.q = Q; r.nb = nb;
+      tab[lane / K] = r;
+    }
+  }
+  __syncthreads();
+
+  // ---- producer helpers: wave w (0, 1) owns rows [256 w, 256 w + 256), 16 rows per access
+  const uint32_t pw = wave - 8u, pl = tid & 63u;
+  // global byte address of chunk (row, c) of round t, or 0 when the chunk carries no payload;
+  // `full` = the whole 16 B lie inside the packet's buffer range and are 16-B aligned
+  auto chunk_addr = [&](uint32_t row, uint32_t c, uint32_t t, bool out, uint32_t& nbytes) -> uint64_t {
+    const WsPkt r = tab[row / K];
+    nbytes = 0;
+    if (!(r.flags & 1u)) return 0;
+    const uint32_t hh = row % K, rb0 = hh * r.q;
+    if (rb0 >= r.nb) return 0;
+    const uint32_t rnr = min(r.q, r.nb - rb0);
+    const uint32_t b = rb0 + t;
+    if (t >= rnr || b == 0) return 0;
+    const uint32_t coff = 64u * (b - 1u) + 16u * c;
+    if (coff >= r.len) return 0;
+    nbytes = min(16u, r.len - coff);
+    const uint64_t base = out ? ((uint64_t)r.out_lo | ((uint64_t)r.out_hi << 32))
+                              : ((uint64_t)r.in_lo | ((uint64_t)r.in_hi << 32));
+    if (!(r.flags & 2u)) nbytes |= 0x100u;  // unaligned packet: byte-wise path
+    return base + coff;
+  };
+  auto produce_loads = [&](uint32_t t) {
+    uint4* buf = rows[t & 1u];
+#pragma unroll 4
+    for (uint32_t i = 0; i < 16; ++i) {
+      const uint32_t R = 256u * pw + 16u * i, row = R + (pl >> 2), sl = pl & 3u;
+      const uint32_t c = (sl - (row >> 2)) & 3u;
+      uint32_t nbytes;
+      const uint64_t a = chunk_addr(row, c, t, false, nbytes);
+      if (a != 0 && nbytes == 16u) {
+        __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)a, (void*)&buf[4u * R], 16, 0, 0);
+      } else if (a != 0) {  // tail or unaligned chunk: bytes, zero padded
+        const gu8* q = (const gu8*)(uintptr_t)a;
+        const uint32_t n = nbytes & 0xffu;
+        uint32_t w4[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+          uint32_t v = 0;
+#pragma unroll
+          for (uint32_t bb = 0; bb < 4; ++bb)
+            if (4u * k + bb < n) v |= (uint32_t)q[4u * k + bb] << (8u * bb);
+          w4[k] = v;
+        }
+        buf[4u * R + pl] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      }
+    }
+  };
+  auto produce_stores = [&](uint32_t t) {
+    const uint4* buf = rows[t & 1u];
+#pragma unroll 4
+    for (uint32_t i = 0; i < 16; ++i) {
+      const uint32_t R = 256u * pw + 16u * i, row = R + (pl >> 2), sl = pl & 3u;
+      const uint32_t c = (sl - (row >> 2)) & 3u;
+      uint32_t nbytes;
+      const uint64_t a = chunk_addr(row, c, t, true, nbytes);
+      if (a != 0) {
+        const uint4 v = buf[4u * R + pl];
+        if (nbytes == 16u) {
+          *(gu4*)(uintptr_t)a = v;
+        } else {
+          gu8* q = (gu8*)(uintptr_t)a;
+          const uint32_t n = nbytes & 0xffu, w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (uint32_t k = 0; k < 16; ++k)
+            if (k < n) q[k] = (uint8_t)(w4[k >> 2] >> (8u * (k & 3u)));
+        }
+      }
+    }
+  };
+
+  if (!consumer) {
+    produce_loads(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+
+  uint32_t acc[5] = {0, 0, 0, 0, 0};
+  uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, sv0 = 0, sv1 = 0, sv2 = 0, sv3 = 0;
+  for (uint32_t t = 0; t < T; ++t) {
+    if (consumer) {
+      uint4* buf = rows[t & 1u];
+      const bool act = t < nr;
+      const uint32_t b = b0 + t;
+      const bool data = act && b > 0;
+      const uint32_t off = 64u * (b - 1u);
+      const uint32_t nbytes = data ? min(64u, len - off) : 0u;
+      uint32_t w[16];
+#pragma unroll
+      for (uint32_t c = 0; c < 4; ++c) {
+        const uint4 v = buf[rowpos(lane, c)];
+        w[4 * c] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+      }
+      uint32_t m[16];
+      uint32_t nch = 0;
+      if (act) {
+        uint32_t ks[16];
+        chacha20_block(key, b, ctr_lo, ctr_hi, 0u, ks);
+        if (!data) {
+          r0 = ks[0] & 0x0fffffffu;
+          r1 = ks[1] & 0x0ffffffcu;
+          r2 = ks[2] & 0x0ffffffcu;
+          r3 = ks[3] & 0x0ffffffcu;
+          sv0 = ks[4]; sv1 = ks[5]; sv2 = ks[6]; sv3 = ks[7];
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const uint32_t x = w[i] ^ ks[i];
+            m[i] = MODE == WG_MODE_SEAL ? x : w[i];  // MAC input: the ciphertext
+            w[i] = x;
+          }
+#pragma unroll
+          for (uint32_t c = 0; c < 4; ++c)
+            buf[rowpos(lane, c)] = make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
+          if (nbytes < 64u) mask_block(nbytes, m);
+          nch = (nbytes + 15u) >> 4;
+        }
+      }
+      if (K > 1 && t == 0) {
+        const int sl = (int)((lane & 63u) - h);
+        r0 = __shfl(r0, sl, 64);
+        r1 = __shfl(r1, sl, 64);
+        r2 = __shfl(r2, sl, 64);
+        r3 = __shfl(r3, sl, 64);
+      }
+      const uint32_t s1 = r1 + (r1 >> 2), s2 = r2 + (r2 >> 2), s3 = r3 + (r3 >> 2);
+#pragma unroll
+      for (uint32_t c = 0; c < 4u; ++c)
+        if (c < nch) p32_block(acc, m[4 * c], m[4 * c + 1], m[4 * c + 2], m[4 * c + 3], r0, r1, r2, r3, s1, s2, s3);
+    } else {
+      if (t >= 1u) produce_stores(t - 1u);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the rows are read before they are refilled
+      if (t + 1u < T) produce_loads(t + 1u);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // next round's rows have landed
+    }
+    __syncthreads();
+  }
+  if (!consumer) {
+    if (T >= 1u) produce_stores(T - 1u);
+    return;
+  }
+
+  // ---- consumers: the length block, the K-lane combine and the tag ----
+  const uint32_t h_last = (nb - 1u) / Q;
+  if (valid && h == h_last) {
+    const uint32_t s1 = r1 + (r1 >> 2), s2 = r2 + (r2 >> 2), s3 = r3 + (r3 >> 2);
+    p32_block(acc, 0u, 0u, len, 0u, r0, r1, r2, r3, s1, s2, s3);
+  }
+  uint32_t A[5];
+  poly_block_limbs(acc[0], acc[1], acc[2], acc[3], acc[4] << 24, A);
+  if constexpr (K > 1) {
+    const uint32_t nc = (len + 15u) >> 4;
+    uint32_t e = (valid && h < h_last) ? nc + 5u - 4u * (h + 1u) * Q : 0u;
+    if (__any(e != 0u)) {
+      uint32_t base[5], pwr[5];
+      poly_r_limbs(r0, r1, r2, r3, base);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) pwr[i] = 0;
+      bool have = false;
+      const bool need = e != 0u;
+      while (__any(e != 0u)) {
+        if (e & 1u) {
+          if (have) {
+            mul26(pwr, base);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) pwr[i] = base[i];
+            have = true;
+          }
+        }
+        e >>= 1;
+        if (e != 0u) {
+          uint32_t tmp[5];
+#pragma unroll
+          for (int i = 0; i < 5; ++i) tmp[i] = base[i];
+          mul26(base, tmp);
+        }
+      }
+      if (need) mul26(A, pwr);
+    }
+#pragma unroll
+    for (int sh = 1; sh < K; sh <<= 1) {
+#pragma unroll
+      for (int i = 0; i < 5; ++i) A[i] += __shfl_xor(A[i], sh, 64);
+    }
+  }
+  const uint8_t* src = P.in + in_off;
+  uint8_t* dst = P.out + out_off;
+  uint32_t bad = valid ? 0u : 1u;
+  if (h == 0 && valid) {
+    uint32_t tag[4];
+    poly_finish(A, sv0, sv1, sv2, sv3, tag);
+    if constexpr (MODE == WG_MODE_SEAL) {
+      uint8_t* tp = dst + len;
+      if ((((uintptr_t)tp) & 15u) == 0) {
+        *(uint4*)tp = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) store_u32_any(tp + 4 * i, tag[i]);
+      }
+    } else {
+      const uint8_t* tp = src + len;
+      uint32_t diff = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) diff |= load_u32_any(tp + 4 * i) ^ tag[i];
+      bad = diff ? 1u : 0u;
+    }
+  }
+  if constexpr (MODE == WG_MODE_OPEN) {
+    if constexpr (K > 1) bad = __shfl(bad, (int)((lane & 63u) - h), 64);
+    const bool in_grid = gid < (uint64_t)P.n * K;
+    if (in_grid && h == 0 && P.status) P.status[pkt] = bad ? WG_PKT_BADTAG : WG_PKT_OK;
+  }
+  // OPEN with a bad tag: the producers' stores of this lane's rows may still be in
+  // flight, so the scrub runs in a second launch (k_ws_scrub) ordered after this one
+}
+
+// Zero the plaintext of every packet whose status is BADTAG (k_ws's open leaves it
+// to this launch, which the stream orders after the producers' stores).
+__global__ void __launch_bounds__(256) k_ws_scrub(StreamParams P) {
+  const uint64_t gid = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  const uint32_t pkt = (uint32_t)(gid >> 4), part = (uint32_t)(gid & 15u);
+  if (pkt >= P.n || !P.status || P.status[pkt] != WG_PKT_BADTAG) return;
+  const uint4 lo = ((const uint4*)(P.desc + pkt))[0], hi = ((const uint4*)(P.desc + pkt))[1];
+  const uint64_t in_off = (uint64_t)lo.x | ((uint64_t)lo.y << 32), out_off = (uint64_t)lo.z | ((uint64_t)lo.w << 32);
+  const uint32_t len = hi.z;
+  const bool valid = len <= P.max_len && hi.w < P.key_slots && in_off <= P.in_size &&
+                     (uint64_t)len + 16u <= P.in_size - in_off && out_off <= P.out_size &&
+                     (uint64_t)len <= P.out_size - out_off;
+  if (!valid) return;
+  uint8_t* o = P.out + out_off;
+  for (uint32_t i = part; i < len; i += 16u) o[i] = 0;
+}
+
 }  // namespace wgk
