@@ -104,6 +104,14 @@ int wg_sync(wg_ctx* ctx, void* stream); /* hipStreamSynchronize */
 const char* wg_last_error(void);        /* thread-local text for the last error */
 const char* wg_version(void);
 
+/* Transport kernel used by this context's wg_seal_batch / wg_open_batch / *_host calls
+ * (a tuning and test hook beside the reference interface). name: "default"
+ * or NULL (the process default: WG_TRANSPORT_KERNEL, else k_wave), "wave", "stream",
+ * "tile", "lane", "quad", "coop", "ws", "pipe", "lean"; lanes: lanes per packet for
+ * lane/coop/ws (1, 2, 4 or 8); variant: the kernel's variant bits (0 = its base form).
+ * Every kernel computes identical bytes; they differ only in speed. */
+int wg_ctx_set_kernel(wg_ctx* ctx, const char* name, uint32_t lanes, uint32_t variant);
+
 /* ---- keys: SymmetricKeypair(byte[] send, byte[] recv) and clean() ---------
  * (SymmetricKeypair.java:39-50 copies keys into a shared Arena; :85-93 zeroes them) */
 int wg_keys_set(wg_ctx* ctx, uint32_t first_slot, uint32_t n, const uint8_t* keys_host /* n*32 */);

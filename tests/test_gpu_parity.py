@@ -322,3 +322,52 @@ def test_full_c1_roundtrip(engine, torch_dev):
     mask = np.zeros(S, bool); mask[:L] = True
     m = np.tile(mask, n)
     assert np.array_equal(pt[m], inp[m])
+
+
+# ---- every selectable transport kernel (wg_ctx_set_kernel) --------------------------
+
+KERNELS = [("wave", 1, 5), ("stream", 8, 1), ("tile", 2, 0), ("lane", 2, 5), ("lane", 1, 1), ("lane", 4, 5),
+           ("quad", 4, 0), ("coop", 2, 0), ("coop", 1, 0), ("ws", 2, 0)]
+
+
+@pytest.mark.parametrize("kern,lanes,variant", KERNELS)
+def test_every_transport_kernel_bit_exact(torch_dev, kern, lanes, variant):
+    """each transport kernel seals and opens bit-exact vs the oracle on a
+    uniform 1420-B batch and on a mixed 0..3000-B batch, and rejects a tampered tag
+    (status BADTAG, plaintext scrubbed). k_ws serves uniform batches only; on the mixed
+    batch the context falls back to k_stream."""
+    W = wg()
+    eng = W.Engine(0, key_slots=64)
+    try:
+        eng.set_kernel(kern, lanes, variant)
+        for case, (lengths, uniform) in enumerate([([1420] * 777, True),
+                                                   (list(splitmix_np(11, 4 * 777).view("<u4") % 3001), False)]):
+            n = len(lengths)
+            desc, keys, inp, out_size = make_batch(n, lengths, 64, seed=101 + case)
+            sealed, _ = run_device(eng, torch_dev, desc, keys, inp, out_size, uniform=uniform)
+            ref = np.zeros(out_size, np.uint8)
+            O.seal_batch(desc, inp, ref, keys, threads=8)
+            assert np.array_equal(sealed, ref), (kern, lanes, variant, case)
+            od = desc.copy()
+            od["in_off"], od["out_off"] = desc["out_off"], desc["in_off"]
+            tampered = sealed.copy()
+            tampered[int(desc["out_off"][5]) + int(desc["len"][5])] ^= 0x01
+            pt, st = run_device(eng, torch_dev, od, keys, tampered, len(inp), open_=True, uniform=uniform)
+            exp = np.zeros(n, np.int32)
+            exp[5] = 1
+            assert np.array_equal(st, exp), (kern, case)
+            for i in range(n):
+                o, l = int(desc["in_off"][i]), int(desc["len"][i])
+                want = np.zeros(l, np.uint8) if i == 5 else inp[o:o + l]
+                assert np.array_equal(pt[o:o + l], want), (kern, case, i)
+    finally:
+        eng.close()
+
+
+def test_set_kernel_rejects_unknown_names(engine):
+    W = wg()
+    with pytest.raises(W.WgError):
+        engine.set_kernel("nope", 2, 0)
+    with pytest.raises(W.WgError):
+        engine.set_kernel("lane", 3, 0)
+    engine.set_kernel("default")

@@ -67,6 +67,7 @@ SIGNATURES = [
     ("wg_sync", _I, [_VP, _VP]),
     ("wg_last_error", ctypes.c_char_p, []),
     ("wg_version", ctypes.c_char_p, []),
+    ("wg_ctx_set_kernel", ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32]),
     ("wg_keys_set", _I, [_VP, _U32, _U32, _VP]),
     ("wg_keys_zero", _I, [_VP, _U32, _U32]),
     ("wg_seal_batch", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _U32, _U32, _VP]),

@@ -78,6 +78,10 @@ struct wg_ctx {
   // non-uniform plan workspace
   DevBuf plan_nb, plan_prefix, plan_tiles, plan_ntiles, plan_tmp;
   DevBuf sink;  // k_coop scratch
+  // transport kernel for this context (wg_ctx_set_kernel); kern == 0: the process
+  // default from WG_TRANSPORT_KERNEL (tunables())
+  int kern = 0;
+  uint32_t kern_k = 2, kern_v = 0;
   // host-API staging
   DevBuf h_desc, h_in, h_out, h_aad, h_status, h_keys;
   std::mutex mu;  // serialises host-API calls and plan workspace reuse
@@ -342,6 +346,48 @@ void launch_lane(int K, int V, uint32_t n, hipStream_t s, const wgk::StreamParam
   }
 }
 
+// transport kernels selectable per context (wg_ctx_set_kernel) or per process
+// (WG_TRANSPORT_KERNEL); k_wave is the default
+enum Kern { KERN_DEFAULT = 0, KERN_WAVE, KERN_STREAM, KERN_TILE, KERN_LANE, KERN_QUAD, KERN_COOP, KERN_WS, KERN_PIPE, KERN_LEAN };
+struct KernChoice {
+  int kind;
+  uint32_t k;     // lanes per packet (lane, coop, ws)
+  int v_seal;     // variant bits (wave: per mode)
+  int v_open;
+};
+int kern_from_name(const char* e) {
+  if (!e || !strcmp(e, "default") || !strcmp(e, "wave")) return KERN_WAVE;
+  if (!strcmp(e, "stream")) return KERN_STREAM;
+  if (!strcmp(e, "tile")) return KERN_TILE;
+  if (!strcmp(e, "lane")) return KERN_LANE;
+  if (!strcmp(e, "quad")) return KERN_QUAD;
+  if (!strcmp(e, "coop")) return KERN_COOP;
+  if (!strcmp(e, "ws")) return KERN_WS;
+  if (!strcmp(e, "pipe")) return KERN_PIPE;
+  if (!strcmp(e, "lean")) return KERN_LEAN;
+  return -1;
+}
+KernChoice kern_choice(const wg_ctx* c) {
+  const Tunables& T = tunables();
+  if (c->kern != KERN_DEFAULT) {
+    const int v = (int)c->kern_v;
+    return {c->kern, c->kern_k, v, v};
+  }
+  int kind = KERN_STREAM;
+  if (T.use_tile_for_transport) kind = KERN_TILE;
+  else if (T.use_ws) kind = KERN_WS;
+  else if (T.use_coop) kind = KERN_COOP;
+  else if (T.use_quad) kind = KERN_QUAD;
+  else if (T.use_lane) kind = KERN_LANE;
+  else if (T.use_wave) kind = KERN_WAVE;
+  else if (T.use_lean) kind = KERN_LEAN;
+  else if (T.use_pipe) kind = KERN_PIPE;
+  if (kind == KERN_WAVE) return {kind, 1u, T.wave_variant, T.wave_variant_open};
+  if (kind == KERN_QUAD) return {kind, 4u, T.quad_variant, T.quad_variant};
+  if (kind == KERN_STREAM) return {kind, 8u, T.stream_variant, T.stream_variant};
+  return {kind, (uint32_t)T.lane_k, T.lane_variant, T.lane_variant};
+}
+
 // the caller's stream as-is: NULL is HIP's default (null) stream, like every HIP API;
 // pass wg_ctx_stream(ctx) to use the context's own non-blocking stream
 // Transport seal/open through k_stream (one wave per workgroup, 8 packet slots).
@@ -367,7 +413,10 @@ int launch_stream(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
 #ifdef WG_DIAG
   P.stamps = g_stamps;
 #endif
-  if (tunables().use_coop) {
+  const KernChoice ch = kern_choice(c);
+  const int CV = MODE == WG_MODE_OPEN ? ch.v_open : ch.v_seal;
+  const uint32_t K = ch.k == 1 ? 1u : (ch.k == 4 ? 4u : (ch.k == 8 ? 8u : 2u));
+  if (ch.kind == KERN_COOP) {
     int rc;
     if ((rc = c->sink.ensure(wgk::kCoopSinkBytes)) != WG_OK) return rc;
     P.sink = (uint8_t*)c->sink.p;
@@ -376,37 +425,34 @@ int launch_stream(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
   const uint32_t pad = tunables().stream_lds_pad;
   hipEvent_t ev;
   record_start(c, s, &ev);
-  if (tunables().use_ws && (flags & WG_F_UNIFORM)) {
-    const uint32_t K = tunables().lane_k == 1 ? 1u : (tunables().lane_k == 4 ? 4u : 2u);
+  if (ch.kind == KERN_WS && (flags & WG_F_UNIFORM) && K <= 4u) {
     const uint32_t wgrid = (uint32_t)(((uint64_t)n * K + 511u) / 512u);
     if (K == 1) hipLaunchKernelGGL((wgk::k_ws<MODE, 1>), dim3(wgrid), dim3(640), 0, s, P);
     else if (K == 4) hipLaunchKernelGGL((wgk::k_ws<MODE, 4>), dim3(wgrid), dim3(640), 0, s, P);
     else hipLaunchKernelGGL((wgk::k_ws<MODE, 2>), dim3(wgrid), dim3(640), 0, s, P);
     if (MODE == WG_MODE_OPEN && status)
       hipLaunchKernelGGL(wgk::k_ws_scrub, dim3((uint32_t)(((uint64_t)n * 16u + 255u) / 256u)), dim3(256), 0, s, P);
-  } else if (tunables().use_coop) {
-    const uint32_t K = tunables().lane_k == 1 ? 1u : (tunables().lane_k == 4 ? 4u : 2u);
+  } else if (ch.kind == KERN_COOP && K <= 4u) {
     const uint32_t cgrid = (uint32_t)(((uint64_t)n * K + 63u) / 64u);
-    const int CV = tunables().lane_variant;
     if (K == 2 && CV == 8) hipLaunchKernelGGL((wgk::k_coop<MODE, 2, 8>), dim3(cgrid), dim3(64), 0, s, P);
     else if (K == 2 && CV == 48) hipLaunchKernelGGL((wgk::k_coop<MODE, 2, 48>), dim3(cgrid), dim3(64), 0, s, P);
     else if (K == 2 && CV == 16) hipLaunchKernelGGL((wgk::k_coop<MODE, 2, 16>), dim3(cgrid), dim3(64), 0, s, P);
     else if (K == 1) hipLaunchKernelGGL((wgk::k_coop<MODE, 1, 0>), dim3(cgrid), dim3(64), 0, s, P);
     else if (K == 4) hipLaunchKernelGGL((wgk::k_coop<MODE, 4, 0>), dim3(cgrid), dim3(64), 0, s, P);
     else hipLaunchKernelGGL((wgk::k_coop<MODE, 2, 0>), dim3(cgrid), dim3(64), 0, s, P);
-  } else if (tunables().use_quad) {
+  } else if (ch.kind == KERN_QUAD) {
     const uint32_t qgrid = (uint32_t)(((uint64_t)n * 4u + 63u) / 64u);
-    switch (tunables().quad_variant) {
+    switch (CV) {
       case 2: hipLaunchKernelGGL((wgk::k_quad<MODE, 2>), dim3(qgrid), dim3(64), 0, s, P); break;
       case 16: hipLaunchKernelGGL((wgk::k_quad<MODE, 16>), dim3(qgrid), dim3(64), 0, s, P); break;
       case 48: hipLaunchKernelGGL((wgk::k_quad<MODE, 48>), dim3(qgrid), dim3(64), 0, s, P); break;
       default: hipLaunchKernelGGL((wgk::k_quad<MODE, 0>), dim3(qgrid), dim3(64), 0, s, P); break;
     }
-  } else if (tunables().use_lane) {
-    launch_lane<MODE>(tunables().lane_k, tunables().lane_variant, n, s, P);
-  } else if (tunables().use_wave) {
+  } else if (ch.kind == KERN_LANE) {
+    launch_lane<MODE>((int)K, CV, n, s, P);
+  } else if (ch.kind == KERN_WAVE) {
     const int G = tunables().wave_wpg;
-    const int V = MODE == WG_MODE_OPEN ? tunables().wave_variant_open : tunables().wave_variant;
+    const int V = CV;
     const uint32_t wgrid = (grid + G - 1) / G;
     switch (G) {
       case 4: launch_wave<MODE, 4>(V, wgrid, s, P); break;
@@ -414,16 +460,16 @@ int launch_stream(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
       case 16: launch_wave<MODE, 16>(V, wgrid, s, P); break;
       default: launch_wave<MODE, 1>(V, wgrid, s, P); break;
     }
-  } else if (tunables().use_lean) {
+  } else if (ch.kind == KERN_LEAN) {
     hipLaunchKernelGGL((wgk::k_lean<MODE>), dim3(grid), dim3(64), 0, s, P);
-  } else if (tunables().use_pipe) {
+  } else if (ch.kind == KERN_PIPE) {
     hipLaunchKernelGGL((wgk::k_pipe<MODE, 0>), dim3(grid), dim3(64), 0, s, P);
-  } else switch (tunables().stream_variant) {
+  } else switch (ch.kind == KERN_STREAM ? CV : tunables().stream_variant) {
 #define WG_CASE(V) \
   case V: hipLaunchKernelGGL((wgk::k_stream<MODE, V>), dim3(grid), dim3(64), pad, s, P); break;
     WG_CASE(0) WG_CASE(1) WG_CASE(2) WG_CASE(3) WG_CASE(4) WG_CASE(5) WG_CASE(6) WG_CASE(7)
     WG_CASE(9) WG_CASE(11) WG_CASE(15) WG_CASE(17) WG_CASE(33) WG_CASE(49) WG_CASE(65) WG_CASE(73)
-    default: return fail(WG_EINVAL, "WG_STREAM_VARIANT %d not built", tunables().stream_variant);
+    default: return fail(WG_EINVAL, "k_stream variant %d not built", ch.kind == KERN_STREAM ? CV : tunables().stream_variant);
 #undef WG_CASE
   }
   hipError_t e = hipGetLastError();
@@ -435,7 +481,7 @@ int launch_stream(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
 template <int MODE>
 int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, uint64_t in_size, uint8_t* out,
                      uint64_t out_size, uint32_t* status, uint32_t max_len, uint32_t flags, hipStream_t s) {
-  if (tunables().use_tile_for_transport)
+  if (kern_choice(c).kind == KERN_TILE)
     return launch_tiles<MODE, false>(c, desc, n, in, in_size, nullptr, 0, out, out_size, status, max_len, flags, s);
   return launch_stream<MODE>(c, desc, n, in, in_size, out, out_size, status, max_len, flags, s);
 }
@@ -456,6 +502,23 @@ int wg_diag_stamps(void* dev_buf) {
 
 const char* wg_last_error(void) { return g_err.c_str(); }
 const char* wg_version(void) { return "wgaead 0.1.0 gfx950"; }
+
+int wg_ctx_set_kernel(wg_ctx* c, const char* name, uint32_t lanes, uint32_t variant) {
+  if (!c) return fail(WG_EINVAL, "ctx is NULL");
+  if (!name || !strcmp(name, "default")) {
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->kern = KERN_DEFAULT;
+    return WG_OK;
+  }
+  const int k = kern_from_name(name);
+  if (k < 0) return fail(WG_EINVAL, "unknown transport kernel '%s'", name);
+  if (lanes != 1 && lanes != 2 && lanes != 4 && lanes != 8) return fail(WG_EINVAL, "lanes per packet must be 1, 2, 4 or 8");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->kern = k;
+  c->kern_k = lanes;
+  c->kern_v = variant;
+  return WG_OK;
+}
 
 int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   if (!out) return fail(WG_EINVAL, "out is NULL");

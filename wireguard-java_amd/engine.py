@@ -71,6 +71,11 @@ class Engine:
         except Exception:
             pass
 
+    def set_kernel(self, name: str | None = "default", lanes: int = 2, variant: int = 0) -> None:
+        """Transport kernel for this engine's seal/open calls (wg_ctx_set_kernel); every
+        kernel computes the same bytes, only the speed differs."""
+        L.check(self._lib.wg_ctx_set_kernel(self.ctx, None if name is None else name.encode(), lanes, variant))
+
     @property
     def stream(self) -> int:
         return self._lib.wg_ctx_stream(self.ctx)
