@@ -226,8 +226,9 @@ def test_transport_golden_vectors_on_device(engine, torch_dev):
 
 
 def test_mixed_sizes_many_keys(engine, torch_dev):
-    """C2 shape at reduced n: lengths 64..9000, 256 session keys, per-packet key/nonce gather."""
-    n = 3000
+    """C2 shape at reduced n: lengths 64..9000, 256 session keys, per-packet key/nonce gather;
+    two tampered tags among 6000 packets come back BADTAG with their plaintext scrubbed."""
+    n = 6000
     lengths = 64 + splitmix_np(77, 4 * n).view("<u4") % (9000 - 64 + 1)
     desc, keys, inp, out_size = make_batch(n, lengths, 256, seed=5)
     sealed, _ = run_device(engine, torch_dev, desc, keys, inp, out_size)
@@ -236,11 +237,18 @@ def test_mixed_sizes_many_keys(engine, torch_dev):
     assert np.array_equal(sealed, ref)
     od = desc.copy()
     od["in_off"], od["out_off"] = desc["out_off"], desc["in_off"]
-    pt, st = run_device(engine, torch_dev, od, keys, sealed, len(inp), open_=True)
-    assert not st.any()
-    for i in range(0, n, 7):
+    tampered = sealed.copy()
+    bad = [123, 4321]
+    for i in bad:
+        tampered[int(desc["out_off"][i]) + int(desc["len"][i])] ^= 0x80
+    pt, st = run_device(engine, torch_dev, od, keys, tampered, len(inp), open_=True)
+    exp = np.zeros(n, np.int32)
+    exp[bad] = 1
+    assert np.array_equal(st, exp)
+    for i in list(range(0, n, 7)) + bad:
         o, l = int(desc["in_off"][i]), int(desc["len"][i])
-        assert np.array_equal(pt[o:o + l], inp[o:o + l])
+        want = np.zeros(l, np.uint8) if i in bad else inp[o:o + l]
+        assert np.array_equal(pt[o:o + l], want), i
 
 
 def test_unaligned_offsets_and_lengths(engine, torch_dev):
