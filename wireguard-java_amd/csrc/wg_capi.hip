@@ -416,7 +416,7 @@ int launch_stream(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
   const KernChoice ch = kern_choice(c);
   const int CV = MODE == WG_MODE_OPEN ? ch.v_open : ch.v_seal;
   const uint32_t K = ch.k == 1 ? 1u : (ch.k == 4 ? 4u : (ch.k == 8 ? 8u : 2u));
-  if (ch.kind == KERN_COOP) {
+  if (ch.kind == KERN_COOP || ch.kind == KERN_WS) {
     int rc;
     if ((rc = c->sink.ensure(wgk::kCoopSinkBytes)) != WG_OK) return rc;
     P.sink = (uint8_t*)c->sink.p;

@@ -872,7 +872,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
 }
 
 // ---------------------------------------------------------------------------
-// k_ws — warp-specialised transport kernel: k_lane's contiguous block ranges computed
+// k_ws — warp-specialised transport kernel (three LDS rounds in flight): k_lane's contiguous block ranges computed
 // by 8 consumer waves out of LDS while 2 producer waves move the payload between HBM
 // and LDS, so the ARX rounds and the payload stream run at the same time instead of
 // taking turns inside every wave. One workgroup = 10 waves; the
@@ -897,7 +897,7 @@ __global__ void __launch_bounds__(640) k_ws(StreamParams P) {
   static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
   static_assert(K == 1 || K == 2 || K == 4, "lanes per packet");
   constexpr uint32_t NC = 512, NPK = NC / K;  // consumer lanes, packets per workgroup
-  __shared__ uint4 rows[2][NC * 4];           // 2 x 32 KB
+  __shared__ uint4 rows[3][NC * 4];           // 3 x 32 KB: rounds t (consumers), t+1 (landed), t+2 (in flight)
   __shared__ WsPkt tab[NPK];
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -975,17 +975,33 @@ __global__ void __launch_bounds__(640) k_ws(StreamParams P) {
     if (!(r.flags & 2u)) nbytes |= 0x100u;  // unaligned packet: byte-wise path
     return base + coff;
   };
+  // every producer lane issues exactly 16 LDS-DMA loads per round (a chunk without
+  // payload reads the sink), so "round t+1 has landed" is s_waitcnt vmcnt(16) while
+  // round t+2 is in flight; chunks the DMA cannot take (unaligned packet, or a tail
+  // chunk whose 16-B over-read would leave the input buffer) are patched afterwards
+  const uint64_t in_end = (uint64_t)(uintptr_t)P.in + P.in_size;
+  const uint8_t* sinkp = P.sink + 16u * pl;
+  auto dma_ok = [&](uint64_t a, uint32_t nbytes) { return a != 0 && !(nbytes & 0x100u) && a + 16u <= in_end; };
   auto produce_loads = [&](uint32_t t) {
-    uint4* buf = rows[t & 1u];
+    uint4* buf = rows[t % 3u];
 #pragma unroll 4
     for (uint32_t i = 0; i < 16; ++i) {
       const uint32_t R = 256u * pw + 16u * i, row = R + (pl >> 2), sl = pl & 3u;
       const uint32_t c = (sl - (row >> 2)) & 3u;
       uint32_t nbytes;
       const uint64_t a = chunk_addr(row, c, t, false, nbytes);
-      if (a != 0 && nbytes == 16u) {
-        __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)a, (void*)&buf[4u * R], 16, 0, 0);
-      } else if (a != 0) {  // tail or unaligned chunk: bytes, zero padded
+      const void* g = dma_ok(a, nbytes) ? (const void*)(uintptr_t)a : (const void*)sinkp;
+      __builtin_amdgcn_global_load_lds(g, (void*)&buf[4u * R], 16, 0, 0);
+    }
+  };
+  auto produce_fixups = [&](uint32_t t) {
+    uint4* buf = rows[t % 3u];
+    for (uint32_t i = 0; i < 16; ++i) {
+      const uint32_t R = 256u * pw + 16u * i, row = R + (pl >> 2), sl = pl & 3u;
+      const uint32_t c = (sl - (row >> 2)) & 3u;
+      uint32_t nbytes;
+      const uint64_t a = chunk_addr(row, c, t, false, nbytes);
+      if (a != 0 && !dma_ok(a, nbytes)) {  // bytes, zero padded
         const gu8* q = (const gu8*)(uintptr_t)a;
         const uint32_t n = nbytes & 0xffu;
         uint32_t w4[4];
@@ -1002,7 +1018,7 @@ __global__ void __launch_bounds__(640) k_ws(StreamParams P) {
     }
   };
   auto produce_stores = [&](uint32_t t) {
-    const uint4* buf = rows[t & 1u];
+    const uint4* buf = rows[t % 3u];
 #pragma unroll 4
     for (uint32_t i = 0; i < 16; ++i) {
       const uint32_t R = 256u * pw + 16u * i, row = R + (pl >> 2), sl = pl & 3u;
@@ -1026,7 +1042,13 @@ __global__ void __launch_bounds__(640) k_ws(StreamParams P) {
 
   if (!consumer) {
     produce_loads(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (T > 1u) {
+      produce_loads(1);
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // round 0 has landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    produce_fixups(0);
   }
   __syncthreads();
 
@@ -1034,7 +1056,7 @@ __global__ void __launch_bounds__(640) k_ws(StreamParams P) {
   uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, sv0 = 0, sv1 = 0, sv2 = 0, sv3 = 0;
   for (uint32_t t = 0; t < T; ++t) {
     if (consumer) {
-      uint4* buf = rows[t & 1u];
+      uint4* buf = rows[t % 3u];
       const bool act = t < nr;
       const uint32_t b = b0 + t;
       const bool data = act && b > 0;
@@ -1084,9 +1106,14 @@ __global__ void __launch_bounds__(640) k_ws(StreamParams P) {
         if (c < nch) p32_block(acc, m[4 * c], m[4 * c + 1], m[4 * c + 2], m[4 * c + 3], r0, r1, r2, r3, s1, s2, s3);
     } else {
       if (t >= 1u) produce_stores(t - 1u);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the rows are read before they are refilled
-      if (t + 1u < T) produce_loads(t + 1u);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // next round's rows have landed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows t-1 are read before t+2 refills them
+      if (t + 2u < T) {
+        produce_loads(t + 2u);
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // round t+1 has landed, t+2 in flight
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      if (t + 1u < T) produce_fixups(t + 1u);
     }
     __syncthreads();
   }
