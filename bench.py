@@ -22,13 +22,15 @@ works on its own shard — no collective on the data path. The only collectives
 are the timing barrier and the max-over-ranks reduction.
 
 The JSON line also carries:
-  roofline      the transport kernel (k_stream, seal and open launches) against the
+  roofline      the transport kernel (k_wave, seal and open launches) against the
                 8 TB/s HBM peak: achieved = sum(4L + 32) per step / GPU time per step
                 (SURVEY.md §8d), GPU time from HIP events on the launch stream around
                 the timed region; `traffic` = HBM bytes per launch from the committed
                 rocprofv3 PMC summary (profiles/pmc_*.json) when present
   cpu_baseline  the CPU restatement (oracle/liboracle.so, bit-exact to the
                 reference) timed on this host's cores, rank 0, N = 1 only
+Before the W warmup steps every rank runs untimed steps for --ramp-ms (default 150 ms)
+so the GPU clocks have ramped before the timed region (ramp_ms in the JSON line).
 """
 from __future__ import annotations
 
@@ -124,7 +126,7 @@ def cpu_baseline(lengths, slots, counters, keys, budget_s: float = 1.5):
 
 
 def pmc_valu_insts():
-    """SQ_INSTS_VALU per k_stream launch (mean of seal and open) from the committed PMC summary."""
+    """SQ_INSTS_VALU per transport-kernel launch (mean of seal and open) from the committed PMC summary."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
     if not files:
         return None
@@ -137,7 +139,7 @@ def pmc_valu_insts():
 
 
 def pmc_traffic():
-    """Per-launch HBM bytes of k_stream (mean of the seal and open launches) from the
+    """Per-launch HBM bytes of the transport kernel (mean of the seal and open launches) from the
     newest committed PMC summary (profiles/pmc_*.json, written by tools/pmc_to_json.py)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
     if not files:
@@ -210,8 +212,12 @@ def host_bench(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    # untimed seal+open steps for at least this long before the warmup steps: the
+    # MI355X raises its clocks over the first tens of ms of load (a 20-step run measured
+    # 961-1027 GiB/s on C1, 1220 once ramped; profiles/r01_kernel_study.md §5)
+    ap.add_argument("--ramp-ms", type=float, default=150.0)
     ap.add_argument("--workload", default="c1", choices=["c1", "c2", "c3", "c4"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-mem", default="pinned", choices=["pinned", "pageable"])
@@ -280,6 +286,13 @@ def main():
                 main_stream.wait_stream(s_)
 
     fork()
+    t_ramp = time.perf_counter()
+    ramp_steps = 0
+    while (time.perf_counter() - t_ramp) * 1e3 < args.ramp_ms:
+        step()
+        ramp_steps += 1
+        if ramp_steps % 16 == 0:
+            torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     join()
@@ -353,6 +366,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "ramp_ms": args.ramp_ms,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
             "higher_is_better": True,
             "scaling": "strong" if args.workload == "c3" else "weak",
