@@ -149,6 +149,33 @@ int wg_aead_batch(wg_ctx* ctx, int mode, const wg_aead_desc* desc_dev, uint32_t 
                   uint64_t in_size, const uint8_t* aad_dev, uint64_t aad_size, uint8_t* out_dev, uint64_t out_size,
                   uint32_t* status_dev, uint32_t max_len, void* stream);
 
+/* ---- transport wire framing on device (device pointers) -------------------
+ * Wire packet = 16-B header {u8 type=4, u8 zero[3], u32 receiver_index (LE),
+ * u64 counter (LE)} followed by ct||tag (TransportPacket.java:18-35).
+ * wg_frame_seal: for each desc[i] writes that header at out[desc[i].out_off - 16]
+ *   with receiver_index = receivers_dev[desc[i].key_slot] and counter =
+ *   desc[i].counter — UnencryptedOutgoingTransport.java:14-18 (type, receiver
+ *   index) plus EncryptedOutgoingTransport.java:11-14 (counter). Packets with
+ *   out_off < 16, a header past out_size or key_slot >= the context's key slots
+ *   are left untouched. Launch it on the same stream as wg_seal_batch.
+ * wg_parse_open: builds open descriptors from received wire packets without a
+ *   host parse (UndecryptedIncomingTransport.java:20-33): wire packet i starts
+ *   at wire_dev[pkt_off_dev[i]] and is pkt_len_dev[i] bytes long; desc_out[i] =
+ *   {in_off = off + 16, out_off = off + pkt_len (plaintext right after the
+ *   ciphertext in the same buffer, :30), counter = header counter, len =
+ *   pkt_len - 32, key_slot = key_slot_dev[i]}. A packet whose type byte is not
+ *   4, that is shorter than 32 bytes, or whose packet + plaintext overruns
+ *   wire_size gets len = WG_LEN_INVALID (wg_open_batch then skips it with
+ *   WG_PKT_BADTAG) and parse_status_dev[i] = WG_PKT_BADHDR (else WG_PKT_OK);
+ *   parse_status_dev may be NULL. desc_out_dev must be 16-byte aligned. */
+#define WG_PKT_BADHDR 2u
+#define WG_LEN_INVALID 0xffffffffu
+int wg_frame_seal(wg_ctx* ctx, const wg_pkt* desc_dev, uint32_t n, const uint32_t* receivers_dev, uint8_t* out_dev,
+                  uint64_t out_size, void* stream);
+int wg_parse_open(wg_ctx* ctx, const uint8_t* wire_dev, uint64_t wire_size, const uint64_t* pkt_off_dev,
+                  const uint32_t* pkt_len_dev, const uint32_t* key_slot_dev, uint32_t n, wg_pkt* desc_out_dev,
+                  uint32_t* parse_status_dev, void* stream);
+
 /* ---- host-buffer entry points (synchronous; stage through pinned memory) --
  * wg_seal1 / wg_open1 back the unchanged per-packet SymmetricKeypair API:
  *   cipher(src, dst): wg_seal1(ctx, send_slot, counter, src, L, dst) with dst of L+16 bytes

@@ -220,6 +220,50 @@ def open_batch(desc: np.ndarray, inp: np.ndarray, out: np.ndarray, keys: np.ndar
 
 
 # ---------------------------------------------------------------------------
+# Transport wire framing (oracle for wg_frame_seal / wg_parse_open)
+
+TRANSPORT_TYPE = 4  # TransportPacket.java:28
+HEADER_SIZE = 16    # HEADER_LAYOUT: u8 type, pad 3, u32 receiver_index, u64 counter (TransportPacket.java:30-35)
+
+
+def transport_header(receiver_index: int, counter: int) -> bytes:
+    """The header UnencryptedOutgoingTransport.java:14-18 (type + receiver index) and
+    EncryptedOutgoingTransport.java:11-14 (counter) leave in front of ct||tag; the
+    JAVA_INT / JAVA_LONG layouts are native order, little-endian on x86-64."""
+    return struct.pack("<BxxxIQ", TRANSPORT_TYPE, receiver_index & 0xFFFFFFFF, counter & 0xFFFFFFFFFFFFFFFF)
+
+
+def frame_headers(desc: np.ndarray, receivers: np.ndarray, out: np.ndarray, key_slots: int) -> None:
+    """Oracle for wg_frame_seal: header at out_off - 16 of every in-range packet."""
+    for p in desc:
+        o, slot = int(p["out_off"]), int(p["key_slot"])
+        if o < HEADER_SIZE or o > len(out) or slot >= key_slots:
+            continue
+        out[o - HEADER_SIZE:o] = np.frombuffer(transport_header(int(receivers[slot]), int(p["counter"])), np.uint8)
+
+
+def parse_wire(wire: np.ndarray, pkt_off: np.ndarray, pkt_len: np.ndarray, key_slot: np.ndarray):
+    """Oracle for wg_parse_open (UndecryptedIncomingTransport.java:20-33): ciphertext
+    length = packet length - 16, plaintext at +16+ctLen (:30), counter from the header
+    (TransportPacket.java:53-55); a wrong type byte is rejected (:24-26). Returns
+    (desc, parse_status) with len = 0xFFFFFFFF and status 2 for rejected packets."""
+    n = len(pkt_off)
+    desc = np.zeros(n, WG_PKT)
+    st = np.zeros(n, np.uint32)
+    for i in range(n):
+        o, wl = int(pkt_off[i]), int(pkt_len[i])
+        desc[i]["in_off"], desc[i]["out_off"], desc[i]["key_slot"] = o + 16, o + wl, int(key_slot[i])
+        desc[i]["len"], desc[i]["counter"] = 0xFFFFFFFF, 0
+        ok = wl >= 32 and o + wl + (wl - 32) <= len(wire) and int(wire[o]) == TRANSPORT_TYPE
+        if ok:
+            desc[i]["counter"] = struct.unpack_from("<Q", wire[o + 8:o + 16].tobytes())[0]
+            desc[i]["len"] = wl - 32
+        else:
+            st[i] = 2
+    return desc, st
+
+
+# ---------------------------------------------------------------------------
 # OpenSSL cross-check (independent implementation; not the reference)
 
 _SSL = None

@@ -22,6 +22,8 @@ WG_EDEVICE = -5
 WG_ESELFTEST = -74
 WG_PKT_OK = 0
 WG_PKT_BADTAG = 1
+WG_PKT_BADHDR = 2
+WG_LEN_INVALID = 0xFFFFFFFF
 WG_TAG_SIZE = 16
 WG_NONCE_SIZE = 12
 WG_KEY_SIZE = 32
@@ -72,6 +74,8 @@ SIGNATURES = [
     ("wg_keys_zero", _I, [_VP, _U32, _U32]),
     ("wg_seal_batch", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _U32, _U32, _VP]),
     ("wg_open_batch", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _VP, _U32, _U32, _VP]),
+    ("wg_frame_seal", _I, [_VP, _VP, _U32, _VP, _VP, _U64, _VP]),
+    ("wg_parse_open", _I, [_VP, _VP, _U64, _VP, _VP, _VP, _U32, _VP, _VP, _VP]),
     ("wg_aead_batch", _I, [_VP, _I, _VP, _U32, _VP, _U64, _VP, _U64, _VP, _U64, _VP, _U32, _VP]),
     ("wg_seal1", _I, [_VP, _U32, _U64, _VP, _U32, _VP]),
     ("wg_open1", _I, [_VP, _U32, _U64, _VP, _U32, _VP]),

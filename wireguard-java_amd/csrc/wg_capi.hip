@@ -488,6 +488,71 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
 
 hipStream_t pick_stream(wg_ctx*, void* stream) { return (hipStream_t)stream; }
 
+// ---- wire framing (TransportPacket.java:18-35) ------------------------------
+// One thread per packet: 16 header bytes against ~1.4 KB of AEAD work, so these
+// are launch-bound, not bandwidth-bound; bytes are moved with 4-B or 1-B vector
+// stores depending on the header's alignment (stride 1452 leaves it 4-aligned).
+__device__ inline void put_header(uint8_t* h, uint32_t rx, uint64_t ctr) {
+  const uint32_t w[4] = {4u, rx, (uint32_t)ctr, (uint32_t)(ctr >> 32)};
+  if ((((uintptr_t)h) & 3u) == 0) {
+    uint32_t* h32 = (uint32_t*)h;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) h32[k] = w[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) h[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+  }
+}
+
+__global__ void __launch_bounds__(256) k_frame_seal(const wg_pkt* __restrict__ d, uint32_t n,
+                                                    const uint32_t* __restrict__ rx, uint32_t slots,
+                                                    uint8_t* __restrict__ out, uint64_t out_size) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const wg_pkt p = d[i];
+  if (p.out_off < 16 || p.out_off > out_size || p.key_slot >= slots) return;
+  put_header(out + p.out_off - 16, rx[p.key_slot], p.counter);
+}
+
+__global__ void __launch_bounds__(256) k_parse_open(const uint8_t* __restrict__ wire, uint64_t wire_size,
+                                                    const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
+                                                    const uint32_t* __restrict__ slot, uint32_t n,
+                                                    wg_pkt* __restrict__ d, uint32_t* __restrict__ st) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t o = off[i];
+  const uint32_t wl = len[i];
+  wg_pkt p;
+  p.in_off = o + 16;
+  p.out_off = o + wl;
+  p.key_slot = slot[i];
+  p.counter = 0;
+  p.len = WG_LEN_INVALID;
+  // packet [o, o+wl) plus its plaintext [o+wl, o+2wl-32) must lie inside the buffer
+  bool ok = wl >= 32 && o <= wire_size && (uint64_t)wl <= wire_size - o &&
+            (uint64_t)wl - 32 <= wire_size - o - wl;
+  if (ok) {
+    const uint8_t* h = wire + o;
+    uint32_t w[4];
+    if ((((uintptr_t)h) & 3u) == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[k] = ((const uint32_t*)h)[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        w[k] = (uint32_t)h[4 * k] | ((uint32_t)h[4 * k + 1] << 8) | ((uint32_t)h[4 * k + 2] << 16) |
+               ((uint32_t)h[4 * k + 3] << 24);
+    }
+    ok = (w[0] & 0xffu) == 4u;  // only the type byte is checked (UndecryptedIncomingTransport.java:24-26)
+    if (ok) {
+      p.counter = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+      p.len = wl - 32;
+    }
+  }
+  d[i] = p;
+  if (st) st[i] = ok ? WG_PKT_OK : WG_PKT_BADHDR;
+}
+
 }  // namespace
 
 extern "C" {
@@ -617,6 +682,35 @@ int wg_open_batch(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
   std::lock_guard<std::mutex> lk(c->mu);
   return launch_transport<WG_MODE_OPEN>(c, desc, n, in, in_size, out, out_size, status, max_len, flags,
                                        pick_stream(c, stream));
+}
+
+int wg_frame_seal(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint32_t* receivers, uint8_t* out,
+                  uint64_t out_size, void* stream) {
+  if (!c) return fail(WG_EINVAL, "NULL context");
+  if (n == 0) return WG_OK;
+  if (!desc || !receivers || !out) return fail(WG_EINVAL, "NULL descriptor, receiver table or output buffer");
+  DeviceGuard g(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  hipLaunchKernelGGL(k_frame_seal, dim3((n + 255u) / 256u), dim3(256), 0, s, desc, n, receivers, c->key_slots, out,
+                     out_size);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(WG_EDEVICE, "k_frame_seal launch: %s", hipGetErrorString(e));
+  return WG_OK;
+}
+
+int wg_parse_open(wg_ctx* c, const uint8_t* wire, uint64_t wire_size, const uint64_t* pkt_off, const uint32_t* pkt_len,
+                  const uint32_t* key_slot, uint32_t n, wg_pkt* desc_out, uint32_t* parse_status, void* stream) {
+  if (!c) return fail(WG_EINVAL, "NULL context");
+  if (n == 0) return WG_OK;
+  if (!wire || !pkt_off || !pkt_len || !key_slot) return fail(WG_EINVAL, "NULL wire buffer or packet table");
+  if (!desc_out || (((uintptr_t)desc_out) & 15u)) return fail(WG_EINVAL, "descriptor output must be non-NULL and 16-byte aligned");
+  DeviceGuard g(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  hipLaunchKernelGGL(k_parse_open, dim3((n + 255u) / 256u), dim3(256), 0, s, wire, wire_size, pkt_off, pkt_len,
+                     key_slot, n, desc_out, parse_status);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(WG_EDEVICE, "k_parse_open launch: %s", hipGetErrorString(e));
+  return WG_OK;
 }
 
 int wg_aead_batch(wg_ctx* c, int mode, const wg_aead_desc* desc, uint32_t n, const uint8_t* in, uint64_t in_size,

@@ -120,6 +120,25 @@ class Engine:
                                         out.numel(), status.data_ptr(), max_len, L.WG_F_UNIFORM if uniform else 0,
                                         stream if stream is not None else _torch_stream()))
 
+    def frame_seal(self, desc, receivers, out, stream: int | None = None):
+        """wg_frame_seal: write the 16-B transport header {4, 0, 0, 0, receiver_index, counter}
+        in front of every sealed packet (UnencryptedOutgoingTransport.java:14-18,
+        EncryptedOutgoingTransport.java:11-14). `receivers` is a uint32/int32 device tensor
+        indexed by key slot."""
+        n = desc.shape[0]
+        L.check(self._lib.wg_frame_seal(self.ctx, desc.data_ptr(), n, receivers.data_ptr(), out.data_ptr(),
+                                        out.numel(), stream if stream is not None else _torch_stream()))
+
+    def parse_open(self, wire, pkt_off, pkt_len, key_slot, desc_out, parse_status=None, stream: int | None = None):
+        """wg_parse_open: open descriptors from received wire packets on device
+        (UndecryptedIncomingTransport.java:20-33); plaintext lands right after each
+        packet's ciphertext in `wire`. pkt_off int64, pkt_len / key_slot int32 device tensors."""
+        n = pkt_off.shape[0]
+        L.check(self._lib.wg_parse_open(self.ctx, wire.data_ptr(), wire.numel(), pkt_off.data_ptr(),
+                                        pkt_len.data_ptr(), key_slot.data_ptr(), n, desc_out.data_ptr(),
+                                        parse_status.data_ptr() if parse_status is not None else None,
+                                        stream if stream is not None else _torch_stream()))
+
     def aead(self, mode: int, desc, inp, aad, out, status, max_len: int, stream: int | None = None):
         """wg_aead_batch over torch tensors: desc int64 [n, 8] (wg_aead_desc records)."""
         n = desc.shape[0]

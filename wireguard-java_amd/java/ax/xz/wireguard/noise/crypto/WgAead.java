@@ -26,11 +26,11 @@ public final class WgAead {
 	public static final int WG_OK = 0;
 	public static final int WG_MODE_SEAL = 0, WG_MODE_OPEN = 1, WG_MODE_CIPHER = 2, WG_MODE_MAC = 3;
 	public static final int WG_F_UNIFORM = 1;
-	public static final int WG_PKT_OK = 0, WG_PKT_BADTAG = 1;
+	public static final int WG_PKT_OK = 0, WG_PKT_BADTAG = 1, WG_PKT_BADHDR = 2;
 	public static final long AEAD_DESC_SIZE = 64, PKT_DESC_SIZE = 32;
 
 	static final MethodHandle SELFTEST, CTX_CREATE, LAST_ERROR, KEYS_SET, KEYS_ZERO, SEAL1, OPEN1, AEAD_HOST,
-		SEAL_BATCH, OPEN_BATCH, SYNC, SEAL_HOST, OPEN_HOST, HOST_ALLOC, HOST_FREE;
+		SEAL_BATCH, OPEN_BATCH, SYNC, SEAL_HOST, OPEN_HOST, HOST_ALLOC, HOST_FREE, FRAME_SEAL, PARSE_OPEN;
 
 	/** The process-wide context (one HIP device, its stream and its device key table). */
 	static final MemorySegment CTX;
@@ -57,6 +57,11 @@ public final class WgAead {
 		OPEN_BATCH = down(linker, symbols, "wg_open_batch", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT,
 			ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS, JAVA_INT, JAVA_INT, ADDRESS));
 		SYNC = down(linker, symbols, "wg_sync", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS));
+		// device-side wire framing (TransportPacket.java:18-35): header write on seal, header parse on open
+		FRAME_SEAL = down(linker, symbols, "wg_frame_seal", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT,
+			ADDRESS, ADDRESS, JAVA_LONG, ADDRESS));
+		PARSE_OPEN = down(linker, symbols, "wg_parse_open", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG,
+			ADDRESS, ADDRESS, ADDRESS, JAVA_INT, ADDRESS, ADDRESS, ADDRESS));
 		SEAL_HOST = down(linker, symbols, "wg_seal_host", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT,
 			ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, JAVA_INT, JAVA_INT));
 		OPEN_HOST = down(linker, symbols, "wg_open_host", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT,
