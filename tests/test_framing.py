@@ -140,3 +140,12 @@ def test_device_frame_seal_and_parse_open(engine):
     for i in good[:200] + good[-200:]:
         o = int(off[i]) + int(wl[i])
         assert np.array_equal(opened[o:o + int(lens[i])], tun[i * 2048:i * 2048 + int(lens[i])])
+
+
+def test_framing_entry_points_reject_null_context():
+    """Argument checks run before any HIP call, so they hold on a CPU-only host too."""
+    W = wg()
+    lib = W.lib()
+    assert lib.wg_frame_seal(None, None, 1, None, None, 0, None) == W._lib.WG_EINVAL
+    assert lib.wg_parse_open(None, None, 0, None, None, None, 1, None, None, None) == W._lib.WG_EINVAL
+    assert b"context" in lib.wg_last_error()
