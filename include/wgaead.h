@@ -128,6 +128,14 @@ int wg_keys_zero(wg_ctx* ctx, uint32_t first_slot, uint32_t n);
  * desc[i].len == max_len (closed-form tile plan, no device scan); without it
  * the tile plan is built on device (block-count scan). */
 #define WG_F_UNIFORM 1u
+/* WG_F_FRAME (wg_seal_batch only): also write the 16-B transport header at
+ * out_off - 16 of every packet, exactly as wg_frame_seal does, from the receiver
+ * table given to wg_ctx_set_receivers (k_frame_seal launched after the seal kernel
+ * on the same stream). */
+#define WG_F_FRAME 2u
+/* Device array of receiver_index per key slot (key_slots entries, caller-owned,
+ * must outlive the seals that use it); NULL clears it. */
+int wg_ctx_set_receivers(wg_ctx* ctx, const uint32_t* receivers_dev);
 int wg_seal_batch(wg_ctx* ctx, const wg_pkt* desc_dev, uint32_t n, const uint8_t* in_dev, uint64_t in_size,
                   uint8_t* out_dev, uint64_t out_size, uint32_t max_len, uint32_t flags, void* stream);
 int wg_open_batch(wg_ctx* ctx, const wg_pkt* desc_dev, uint32_t n, const uint8_t* in_dev, uint64_t in_size,

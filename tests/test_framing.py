@@ -149,3 +149,46 @@ def test_framing_entry_points_reject_null_context():
     assert lib.wg_frame_seal(None, None, 1, None, None, 0, None) == W._lib.WG_EINVAL
     assert lib.wg_parse_open(None, None, 0, None, None, None, 1, None, None, None) == W._lib.WG_EINVAL
     assert b"context" in lib.wg_last_error()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", ["wave", "stream", "tile"])
+def test_device_seal_with_frame_flag(engine, kernel):
+    """WG_F_FRAME: the seal kernel, then k_frame_seal on the same stream; the same ring
+    bytes whichever transport kernel sealed."""
+    import torch
+    W = wg()
+    dev = torch.device("cuda", 0)
+    n, slot, nkeys = 3000, 1536, 8
+    rng = np.random.default_rng(77)
+    lens = rng.integers(0, 1489, n).astype(np.uint32)
+    keys = splitmix_np(911, 32 * nkeys)
+    tun = splitmix_np(912, n * 1504)
+    desc = np.zeros(n, O.WG_PKT)
+    desc["in_off"] = np.arange(n, dtype=np.uint64) * 1504
+    desc["out_off"] = np.arange(n, dtype=np.uint64) * slot + 16 + (np.arange(n, dtype=np.uint64) % 3)  # 4-B and 1-B aligned headers
+    desc["counter"] = np.arange(n, dtype=np.uint64) * 3 + (1 << 33)
+    desc["len"] = lens
+    desc["key_slot"] = np.arange(n) % nkeys
+    receivers = splitmix_np(913, 4 * engine.key_slots).view("<u4").copy()
+    rt = torch.from_numpy(receivers.view(np.int32)).to(dev)
+    engine.set_keys(0, keys.tobytes())
+    engine.set_kernel(kernel)
+    try:
+        engine.set_receivers(rt)
+        ring = torch.zeros(n * slot + 64, dtype=torch.uint8, device=dev)
+        engine.seal(torch.from_numpy(W.desc_as_int64(desc)).to(dev), torch.from_numpy(tun).to(dev), ring, 1488,
+                    frame=True)
+        torch.cuda.synchronize()
+    finally:
+        engine.set_kernel("default")
+        engine.set_receivers(None)
+    ref = np.zeros(n * slot + 64, np.uint8)
+    O.seal_batch(desc, tun, ref, keys, threads=8)
+    O.frame_headers(desc, receivers, ref, key_slots=engine.key_slots)
+    assert np.array_equal(ring.cpu().numpy(), ref)
+
+
+def test_frame_flag_needs_receiver_table():
+    W = wg()
+    assert W._lib.WG_F_FRAME == 2

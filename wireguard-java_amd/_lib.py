@@ -29,6 +29,7 @@ WG_NONCE_SIZE = 12
 WG_KEY_SIZE = 32
 WG_MAX_PACKET = 65535
 WG_F_UNIFORM = 1
+WG_F_FRAME = 2
 WG_MODE_SEAL, WG_MODE_OPEN, WG_MODE_CIPHER, WG_MODE_MAC = 0, 1, 2, 3
 
 _ERRNAMES = {WG_EINVAL: "EINVAL", WG_ENOMEM: "ENOMEM", WG_ERANGE: "ERANGE", WG_E2BIG: "E2BIG",
@@ -74,6 +75,7 @@ SIGNATURES = [
     ("wg_keys_zero", _I, [_VP, _U32, _U32]),
     ("wg_seal_batch", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _U32, _U32, _VP]),
     ("wg_open_batch", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _VP, _U32, _U32, _VP]),
+    ("wg_ctx_set_receivers", _I, [_VP, _VP]),
     ("wg_frame_seal", _I, [_VP, _VP, _U32, _VP, _VP, _U64, _VP]),
     ("wg_parse_open", _I, [_VP, _VP, _U64, _VP, _VP, _VP, _U32, _VP, _VP, _VP]),
     ("wg_aead_batch", _I, [_VP, _I, _VP, _U32, _VP, _U64, _VP, _U64, _VP, _U64, _VP, _U32, _VP]),

@@ -75,6 +75,7 @@ struct wg_ctx {
   hipEvent_t ev_desc = nullptr, ev_in = nullptr, ev_kernel = nullptr;
   uint32_t key_slots = 0;
   uint32_t* keys = nullptr;  // device key table
+  const uint32_t* receivers = nullptr;  // device receiver_index per key slot (WG_F_FRAME; caller-owned)
   // non-uniform plan workspace
   DevBuf plan_nb, plan_prefix, plan_tiles, plan_ntiles, plan_tmp;
   DevBuf sink;  // k_coop scratch
@@ -492,18 +493,6 @@ hipStream_t pick_stream(wg_ctx*, void* stream) { return (hipStream_t)stream; }
 // One thread per packet: 16 header bytes against ~1.4 KB of AEAD work, so these
 // are launch-bound, not bandwidth-bound; bytes are moved with 4-B or 1-B vector
 // stores depending on the header's alignment (stride 1452 leaves it 4-aligned).
-__device__ inline void put_header(uint8_t* h, uint32_t rx, uint64_t ctr) {
-  const uint32_t w[4] = {4u, rx, (uint32_t)ctr, (uint32_t)(ctr >> 32)};
-  if ((((uintptr_t)h) & 3u) == 0) {
-    uint32_t* h32 = (uint32_t*)h;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) h32[k] = w[k];
-  } else {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) h[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
-  }
-}
-
 __global__ void __launch_bounds__(256) k_frame_seal(const wg_pkt* __restrict__ d, uint32_t n,
                                                     const uint32_t* __restrict__ rx, uint32_t slots,
                                                     uint8_t* __restrict__ out, uint64_t out_size) {
@@ -511,7 +500,7 @@ __global__ void __launch_bounds__(256) k_frame_seal(const wg_pkt* __restrict__ d
   if (i >= n) return;
   const wg_pkt p = d[i];
   if (p.out_off < 16 || p.out_off > out_size || p.key_slot >= slots) return;
-  put_header(out + p.out_off - 16, rx[p.key_slot], p.counter);
+  wgk::put_header(out + p.out_off - 16, rx[p.key_slot], p.counter);
 }
 
 __global__ void __launch_bounds__(256) k_parse_open(const uint8_t* __restrict__ wire, uint64_t wire_size,
@@ -671,8 +660,24 @@ int wg_seal_batch(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
   if (!c) return fail(WG_EINVAL, "NULL context");
   DeviceGuard g(c->device);
   std::lock_guard<std::mutex> lk(c->mu);
-  return launch_transport<WG_MODE_SEAL>(c, desc, n, in, in_size, out, out_size, nullptr, max_len, flags,
-                                       pick_stream(c, stream));
+  if ((flags & WG_F_FRAME) && !c->receivers) return fail(WG_EINVAL, "WG_F_FRAME without a receiver table (wg_ctx_set_receivers)");
+  hipStream_t s = pick_stream(c, stream);
+  const int rc = launch_transport<WG_MODE_SEAL>(c, desc, n, in, in_size, out, out_size, nullptr, max_len, flags, s);
+  // measured: writing the header inside k_wave cost the seal launch +11% (register
+  // pressure at 64 VGPRs), so every kernel gets k_frame_seal after it on the same stream
+  if (rc != WG_OK || !(flags & WG_F_FRAME) || n == 0) return rc;
+  hipLaunchKernelGGL(k_frame_seal, dim3((n + 255u) / 256u), dim3(256), 0, s, desc, n, c->receivers, c->key_slots, out,
+                     out_size);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(WG_EDEVICE, "k_frame_seal launch: %s", hipGetErrorString(e));
+  return WG_OK;
+}
+
+int wg_ctx_set_receivers(wg_ctx* c, const uint32_t* receivers) {
+  if (!c) return fail(WG_EINVAL, "NULL context");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->receivers = receivers;
+  return WG_OK;
 }
 
 int wg_open_batch(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, uint64_t in_size, uint8_t* out,

@@ -545,6 +545,20 @@ struct StreamParams {
   uint8_t* sink;     // k_coop: 1 MiB device scratch that absorbs the masked-off cooperative accesses
 };
 
+// 16-B transport header {u8 4, u8 0[3], u32 receiver_index, u64 counter}, little-endian
+// (TransportPacket.java:18-35), written with 4-B or 1-B vector stores by alignment.
+__device__ inline void put_header(uint8_t* h, uint32_t rx, uint64_t ctr) {
+  const uint32_t w[4] = {4u, rx, (uint32_t)ctr, (uint32_t)(ctr >> 32)};
+  if ((((uintptr_t)h) & 3u) == 0) {
+    uint32_t* h32 = (uint32_t*)h;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) h32[k] = w[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) h[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+  }
+}
+
 // Per-wave phase accounting for k_stream (diagnostic library only): cycles spent
 // starting packets, in ChaCha, in Poly1305 and finishing, plus realtime start/end.
 #ifdef WG_DIAG

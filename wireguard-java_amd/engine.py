@@ -106,11 +106,14 @@ class Engine:
         L.check(self._lib.wg_keys_zero(self.ctx, first_slot, n))
 
     # ---- device-resident batches (torch tensors on this device) -------------------
-    def seal(self, desc, inp, out, max_len: int, uniform: bool = False, stream: int | None = None):
-        """wg_seal_batch over torch tensors: desc int64 [n,4], inp/out uint8 (device)."""
+    def seal(self, desc, inp, out, max_len: int, uniform: bool = False, stream: int | None = None,
+             frame: bool = False):
+        """wg_seal_batch over torch tensors: desc int64 [n,4], inp/out uint8 (device).
+        frame=True also writes each packet's transport header (WG_F_FRAME)."""
         n = desc.shape[0]
+        flags = (L.WG_F_UNIFORM if uniform else 0) | (L.WG_F_FRAME if frame else 0)
         L.check(self._lib.wg_seal_batch(self.ctx, desc.data_ptr(), n, inp.data_ptr(), inp.numel(), out.data_ptr(),
-                                        out.numel(), max_len, L.WG_F_UNIFORM if uniform else 0,
+                                        out.numel(), max_len, flags,
                                         stream if stream is not None else _torch_stream()))
 
     def open(self, desc, inp, out, status, max_len: int, uniform: bool = False, stream: int | None = None):
@@ -119,6 +122,12 @@ class Engine:
         L.check(self._lib.wg_open_batch(self.ctx, desc.data_ptr(), n, inp.data_ptr(), inp.numel(), out.data_ptr(),
                                         out.numel(), status.data_ptr(), max_len, L.WG_F_UNIFORM if uniform else 0,
                                         stream if stream is not None else _torch_stream()))
+
+    def set_receivers(self, receivers) -> None:
+        """wg_ctx_set_receivers: device tensor of receiver_index per key slot for
+        seal(..., frame=True); the tensor must stay alive while seals use it."""
+        self._receivers = receivers
+        L.check(self._lib.wg_ctx_set_receivers(self.ctx, receivers.data_ptr() if receivers is not None else None))
 
     def frame_seal(self, desc, receivers, out, stream: int | None = None):
         """wg_frame_seal: write the 16-B transport header {4, 0, 0, 0, receiver_index, counter}
