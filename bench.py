@@ -222,6 +222,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-mem", default="pinned", choices=["pinned", "pageable"])
     ap.add_argument("--streams", type=int, default=1)
+    ap.add_argument("--kernel", default="default", help="transport kernel (wg_ctx_set_kernel): default|wave1|tile")
     args = ap.parse_args()
     if args.workload == "c4":
         return host_bench(args)
@@ -243,6 +244,7 @@ def main():
     n = len(lengths)
     keys = splitmix_np(0xC0FFEE + rank, 32 * nkeys)
     eng = wg.Engine(local, key_slots=max(nkeys, 1))
+    eng.set_kernel(args.kernel)
     eng.set_keys(0, keys.tobytes())
 
     # layout: packets at 16-byte aligned strides; pt buffer, ct||tag buffer, decrypted pt buffer
@@ -375,7 +377,7 @@ def main():
             "data": "synthetic (random payload in HBM, splitmix64 keys, sequential counters)",
             "config": {"workload": wdesc, "packets_per_gpu": n, "payload_bytes": int(lengths.mean()),
                        "sessions_per_gpu": nkeys, "parallelism": f"dp{world} sharded by session, no collective"},
-            "roofline": {"bound": "hbm", "kernel": "k_wave<SEAL|OPEN>", "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": "k_transport<SEAL|OPEN>" if args.kernel == "default" else args.kernel, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "alg_bytes_per_launch": int(step_alg / 2),
                          "kernel_ms": round(gpu_step_ms / 2, 5), "seal_ms": round(seal_ms, 5),

@@ -79,7 +79,7 @@ typedef struct wg_aead_desc {
   uint32_t aad_len;   /* 0 = no AAD (poly1305AeadEncrypt(key, nonce, ...) overloads) */
   uint32_t key_slot;  /* ChaCha key (AEAD, CIPHER) or 32-byte one-time key (MAC) */
   uint32_t ctr0;      /* CIPHER mode: initial 32-bit block counter (ChaCha20.chacha20(..., counter)) */
-  uint32_t nonce[3];  /* state words 13..15, little-endian (ChaCha20.java:265) */
+  uint32_t nonce[3];  /* state words 13..15, little-endian (ChaCha20.java:73) */
   uint32_t _reserved[3];
 } wg_aead_desc;
 
@@ -105,11 +105,11 @@ const char* wg_last_error(void);        /* thread-local text for the last error 
 const char* wg_version(void);
 
 /* Transport kernel used by this context's wg_seal_batch / wg_open_batch / *_host calls
- * (a tuning and test hook beside the reference interface). name: "default"
- * or NULL (the process default: WG_TRANSPORT_KERNEL, else k_wave), "wave", "stream",
- * "tile", "lane", "quad", "coop", "ws", "pipe", "lean"; lanes: lanes per packet for
- * lane/coop/ws (1, 2, 4 or 8); variant: the kernel's variant bits (0 = its base form).
- * Every kernel computes identical bytes; they differ only in speed. */
+ * (a test and A/B hook beside the reference interface). name: "default"
+ * or NULL or "transport" (k_transport, the product kernel), "wave1" (the round-1
+ * k_wave kernel, kept as the performance baseline) or "tile" (k_tile, the general
+ * AEAD kernel run on transport descriptors). lanes and variant are ignored (kept for
+ * ABI stability). Every kernel computes identical bytes; they differ only in speed. */
 int wg_ctx_set_kernel(wg_ctx* ctx, const char* name, uint32_t lanes, uint32_t variant);
 
 /* ---- keys: SymmetricKeypair(byte[] send, byte[] recv) and clean() ---------
@@ -124,18 +124,23 @@ int wg_keys_zero(wg_ctx* ctx, uint32_t first_slot, uint32_t n);
  * device against them (an out-of-range packet is skipped with status
  * WG_PKT_BADTAG on open / untouched output on seal, and the call returns 0).
  * `max_len`: every packet's len must be <= max_len (longer ones are treated
- * as out of range); it sizes the LDS tile. Flags: WG_F_UNIFORM promises every
- * desc[i].len == max_len (closed-form tile plan, no device scan); without it
- * the tile plan is built on device (block-count scan). */
+ * as out of range). Flags: WG_F_UNIFORM declares the lengths (nearly) equal: the
+ * packets are taken in order; without it a mixed-length batch is first ordered
+ * longest-first on the device, so every slot of the kernel gets a similar share of
+ * rounds. Unknown flag bits are rejected (WG_EINVAL); wg_open_batch takes only
+ * WG_F_UNIFORM and needs a status array when n > 0. Calls with mixed-length batches
+ * on one context use a shared plan workspace: calls on different streams are ordered
+ * by the library (the later one waits for the earlier one's plan). */
 #define WG_F_UNIFORM 1u
 /* WG_F_FRAME (wg_seal_batch only): also write the 16-B transport header at
  * out_off - 16 of every packet, exactly as wg_frame_seal does, from the receiver
  * table given to wg_ctx_set_receivers (k_frame_seal launched after the seal kernel
  * on the same stream). */
 #define WG_F_FRAME 2u
-/* Device array of receiver_index per key slot (key_slots entries, caller-owned,
- * must outlive the seals that use it); NULL clears it. */
-int wg_ctx_set_receivers(wg_ctx* ctx, const uint32_t* receivers_dev);
+/* Device array of receiver_index per key slot (n >= key_slots entries, device memory
+ * of this context's device, 4-byte aligned, caller-owned, must outlive the seals that
+ * use it); NULL clears it. */
+int wg_ctx_set_receivers(wg_ctx* ctx, const uint32_t* receivers_dev, uint32_t n);
 int wg_seal_batch(wg_ctx* ctx, const wg_pkt* desc_dev, uint32_t n, const uint8_t* in_dev, uint64_t in_size,
                   uint8_t* out_dev, uint64_t out_size, uint32_t max_len, uint32_t flags, void* stream);
 int wg_open_batch(wg_ctx* ctx, const wg_pkt* desc_dev, uint32_t n, const uint8_t* in_dev, uint64_t in_size,
@@ -163,9 +168,11 @@ int wg_aead_batch(wg_ctx* ctx, int mode, const wg_aead_desc* desc_dev, uint32_t 
  * wg_frame_seal: for each desc[i] writes that header at out[desc[i].out_off - 16]
  *   with receiver_index = receivers_dev[desc[i].key_slot] and counter =
  *   desc[i].counter — UnencryptedOutgoingTransport.java:14-18 (type, receiver
- *   index) plus EncryptedOutgoingTransport.java:11-14 (counter). Packets with
- *   out_off < 16, a header past out_size or key_slot >= the context's key slots
- *   are left untouched. Launch it on the same stream as wg_seal_batch.
+ *   index) plus EncryptedOutgoingTransport.java:11-14 (counter). A header is
+ *   written only for the packets the seal accepts (the same test: len <= max_len,
+ *   key_slot < the context's key slots, in_off + len <= in_size, out_off + len + 16
+ *   <= out_size) that also have out_off >= 16; every other packet is left untouched.
+ *   Launch it on the same stream as wg_seal_batch, with the same in_size / max_len.
  * wg_parse_open: builds open descriptors from received wire packets without a
  *   host parse (UndecryptedIncomingTransport.java:20-33): wire packet i starts
  *   at wire_dev[pkt_off_dev[i]] and is pkt_len_dev[i] bytes long; desc_out[i] =
@@ -179,25 +186,37 @@ int wg_aead_batch(wg_ctx* ctx, int mode, const wg_aead_desc* desc_dev, uint32_t 
 #define WG_PKT_BADHDR 2u
 #define WG_LEN_INVALID 0xffffffffu
 int wg_frame_seal(wg_ctx* ctx, const wg_pkt* desc_dev, uint32_t n, const uint32_t* receivers_dev, uint8_t* out_dev,
-                  uint64_t out_size, void* stream);
+                  uint64_t out_size, uint64_t in_size, uint32_t max_len, void* stream);
 int wg_parse_open(wg_ctx* ctx, const uint8_t* wire_dev, uint64_t wire_size, const uint64_t* pkt_off_dev,
                   const uint32_t* pkt_len_dev, const uint32_t* key_slot_dev, uint32_t n, wg_pkt* desc_out_dev,
                   uint32_t* parse_status_dev, void* stream);
 
-/* ---- host-buffer entry points (synchronous; stage through pinned memory) --
+/* ---- host-buffer entry points -----------------------------------------------
  * wg_seal1 / wg_open1 back the unchanged per-packet SymmetricKeypair API:
  *   cipher(src, dst): wg_seal1(ctx, send_slot, counter, src, L, dst) with dst of L+16 bytes
  *   decipher(counter, src, dst): wg_open1(ctx, recv_slot, counter, src, L, dst) with src of L+16 bytes
  *   returns WG_OK, or 1 for a bad tag (dst untouched, as NOISE/crypto/ChaCha20Poly1305.java:51-55).
+ *   Thread-safe and synchronous per call, but batched underneath (the per-packet
+ *   ForkJoinPool fan-out of TransportManager.java:41,79,152-158): the packet is copied
+ *   into the open batch (pinned, device-mapped host memory), a library launcher thread
+ *   seals/opens everything that accumulated while the previous batch ran, and the
+ *   caller returns when its batch completes. Concurrent callers share launches.
+ * wg_batcher_config: at most max_batch packets per launch (1..8192, default 8192) and
+ *   an optional accumulation window (µs after a batch's first packet; default 0 =
+ *   launch as soon as the device is free).
+ * wg_batcher_stats: launches and packets the batcher has issued (mean batch size).
  * wg_seal_host / wg_open_host: a batch in host memory (tun ring in, UDP ring out).
  *   If `in` and `out` are pinned, device-mapped host memory (wg_host_alloc /
  *   wg_host_register) the kernel reads and writes them directly over PCIe
  *   (zero-copy); otherwise the batch moves through device mirrors in chunks with
  *   H2D, kernel and D2H overlapped on three streams. Only packet bytes are written
  *   to `out_host` (bytes between packets — wire headers, ring slack — are kept).
- *   On a bad tag the plaintext range is zero-filled and status[i] = WG_PKT_BADTAG. */
+ *   On a bad tag the plaintext range is zero-filled and status[i] = WG_PKT_BADTAG.
+ *   flags: WG_F_UNIFORM only. */
 int wg_seal1(wg_ctx* ctx, uint32_t key_slot, uint64_t counter, const uint8_t* pt, uint32_t len, uint8_t* out);
 int wg_open1(wg_ctx* ctx, uint32_t key_slot, uint64_t counter, const uint8_t* in, uint32_t len, uint8_t* pt);
+int wg_batcher_config(wg_ctx* ctx, uint32_t max_batch, uint32_t window_us);
+int wg_batcher_stats(wg_ctx* ctx, uint64_t* launches, uint64_t* packets);
 int wg_seal_host(wg_ctx* ctx, const wg_pkt* desc_host, uint32_t n, const uint8_t* in_host, uint64_t in_size,
                  uint8_t* out_host, uint64_t out_size, uint32_t max_len, uint32_t flags);
 int wg_open_host(wg_ctx* ctx, const wg_pkt* desc_host, uint32_t n, const uint8_t* in_host, uint64_t in_size,

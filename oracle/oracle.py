@@ -42,7 +42,7 @@ def _rotl(x: int, n: int) -> int:
 
 
 def py_chacha20_block(key: bytes, counter: int, nonce: bytes) -> bytes:
-    """RFC 8439 2.3 block; state layout as ChaCha20.initializeState (ChaCha20.java:247-266)."""
+    """RFC 8439 2.3 block; state layout as ChaCha20.initializeState (ChaCha20.java:55-74)."""
     s = [0x61707865, 0x3320646E, 0x79622D32, 0x6B206574]
     s += list(struct.unpack("<8I", key))
     s += [counter & 0xFFFFFFFF]
@@ -233,11 +233,18 @@ def transport_header(receiver_index: int, counter: int) -> bytes:
     return struct.pack("<BxxxIQ", TRANSPORT_TYPE, receiver_index & 0xFFFFFFFF, counter & 0xFFFFFFFFFFFFFFFF)
 
 
-def frame_headers(desc: np.ndarray, receivers: np.ndarray, out: np.ndarray, key_slots: int) -> None:
-    """Oracle for wg_frame_seal: header at out_off - 16 of every in-range packet."""
+def frame_headers(desc: np.ndarray, receivers: np.ndarray, out: np.ndarray, key_slots: int,
+                  in_size: int | None = None, max_len: int = 65535) -> None:
+    """Oracle for wg_frame_seal: header at out_off - 16 of every packet the seal accepts
+    (len <= max_len, key slot in the table, input and ct||tag inside their buffers) whose
+    out_off >= 16 (UnencryptedOutgoingTransport.java:14-18, EncryptedOutgoingTransport.java:11-14)."""
     for p in desc:
-        o, slot = int(p["out_off"]), int(p["key_slot"])
-        if o < HEADER_SIZE or o > len(out) or slot >= key_slots:
+        o, slot, L, io = int(p["out_off"]), int(p["key_slot"]), int(p["len"]), int(p["in_off"])
+        if o < HEADER_SIZE or slot >= key_slots or L > max_len:
+            continue
+        if in_size is not None and (io > in_size or L > in_size - io):
+            continue
+        if o > len(out) or L + 16 > len(out) - o:
             continue
         out[o - HEADER_SIZE:o] = np.frombuffer(transport_header(int(receivers[slot]), int(p["counter"])), np.uint8)
 

@@ -9,7 +9,7 @@
  * file:line it follows (paths relative to the reference repository root):
  *   ChaCha20 block        ax.xz.wireguard.noise/src/main/c/chacha-generic.c:10-78
  *   ChaCha20 XOR stream   chacha-generic.c:81-97 (32-bit counter in state word 12)
- *   state layout          ax.xz.wireguard.noise/src/main/java/ax/xz/wireguard/noise/crypto/ChaCha20.java:247-266
+ *   state layout          ax.xz.wireguard.noise/src/main/java/ax/xz/wireguard/noise/crypto/ChaCha20.java:55-74
  *   Poly1305              poly1305-donna.c:26-61, poly1305-donna-64.h:75-223 (restated in radix 2^64)
  *   AEAD composition      .../noise/crypto/ChaCha20Poly1305.java:31-97
  *   transport nonce       .../noise/handshake/SymmetricKeypair.java:52-61 (LE64(counter) || 0^4)
@@ -17,8 +17,9 @@
  *
  * Parity pinning: tests/test_oracle.py checks this file against the RFC 8439
  * vectors held in the reference's own tests (ChaCha20Test.java, Poly1305Test.java),
- * the donna self-test vectors (poly1305-donna.c:83-201) and the fixtures in
- * tests/golden/ generated from the reference C compiled in oracle/_ref/.
+ * the donna self-test vectors (poly1305-donna.c:83-201) and OpenSSL's
+ * EVP_chacha20_poly1305 with the reference nonce layout (tests/golden/, scripts beside
+ * the fixtures). There is no oracle/_ref build of the reference C.
  */
 #include <stdint.h>
 #include <string.h>
@@ -44,10 +45,10 @@ static inline uint32_t rotl(uint32_t x, int n) { return (x << n) | (x >> (32 - n
  * after the block; callers here pass the counter explicitly instead). */
 void oracle_chacha20_block(const uint8_t key[32], uint32_t counter, const uint8_t nonce[12], uint8_t out[64]) {
   uint32_t s[16], x[16];
-  s[0] = 0x61707865u; s[1] = 0x3320646eu; s[2] = 0x79622d32u; s[3] = 0x6b206574u; /* ChaCha20.java:253-256 */
-  for (int i = 0; i < 8; ++i) s[4 + i] = ld32(key + 4 * i);                         /* ChaCha20.java:259 */
-  s[12] = counter;                                                                 /* ChaCha20.java:262 */
-  for (int i = 0; i < 3; ++i) s[13 + i] = ld32(nonce + 4 * i);                      /* ChaCha20.java:265 */
+  s[0] = 0x61707865u; s[1] = 0x3320646eu; s[2] = 0x79622d32u; s[3] = 0x6b206574u; /* ChaCha20.java:61-64 */
+  for (int i = 0; i < 8; ++i) s[4 + i] = ld32(key + 4 * i);                         /* ChaCha20.java:67 */
+  s[12] = counter;                                                                 /* ChaCha20.java:70 */
+  for (int i = 0; i < 3; ++i) s[13 + i] = ld32(nonce + 4 * i);                      /* ChaCha20.java:73 */
   memcpy(x, s, sizeof x);
 #define QR(a, b, c, d)                                   \
   x[a] += x[b]; x[d] = rotl(x[d] ^ x[a], 16);            \

@@ -92,13 +92,13 @@ def test_device_frame_seal_and_parse_open(engine):
     rt = torch.from_numpy(receivers.view(np.int32)).to(dev)
     ring = torch.zeros(n * slot, dtype=torch.uint8, device=dev)
     engine.seal(dt, torch.from_numpy(tun).to(dev), ring, 2032)
-    engine.frame_seal(dt, rt, ring)
+    engine.frame_seal(dt, rt, ring, in_size=tun.size, max_len=2032)
     torch.cuda.synchronize()
     got = ring.cpu().numpy()
 
     ref = np.zeros(n * slot, np.uint8)
     O.seal_batch(desc, tun, ref, keys, threads=8)
-    O.frame_headers(desc, receivers, ref, key_slots=engine.key_slots)
+    O.frame_headers(desc, receivers, ref, key_slots=engine.key_slots, in_size=tun.size, max_len=2032)
     assert np.array_equal(got, ref)
 
     # inbound: tamper 1% of tags, corrupt 3 type bytes, give one packet an overrunning length
@@ -146,13 +146,13 @@ def test_framing_entry_points_reject_null_context():
     """Argument checks run before any HIP call, so they hold on a CPU-only host too."""
     W = wg()
     lib = W.lib()
-    assert lib.wg_frame_seal(None, None, 1, None, None, 0, None) == W._lib.WG_EINVAL
+    assert lib.wg_frame_seal(None, None, 1, None, None, 0, 0, 0, None) == W._lib.WG_EINVAL
     assert lib.wg_parse_open(None, None, 0, None, None, None, 1, None, None, None) == W._lib.WG_EINVAL
     assert b"context" in lib.wg_last_error()
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["wave", "stream", "tile"])
+@pytest.mark.parametrize("kernel", ["transport", "wave1", "tile"])
 def test_device_seal_with_frame_flag(engine, kernel):
     """WG_F_FRAME: the seal kernel, then k_frame_seal on the same stream; the same ring
     bytes whichever transport kernel sealed."""
@@ -185,10 +185,78 @@ def test_device_seal_with_frame_flag(engine, kernel):
         engine.set_receivers(None)
     ref = np.zeros(n * slot + 64, np.uint8)
     O.seal_batch(desc, tun, ref, keys, threads=8)
-    O.frame_headers(desc, receivers, ref, key_slots=engine.key_slots)
+    O.frame_headers(desc, receivers, ref, key_slots=engine.key_slots, in_size=tun.size, max_len=1488)
     assert np.array_equal(ring.cpu().numpy(), ref)
 
 
-def test_frame_flag_needs_receiver_table():
+@pytest.mark.gpu
+def test_frame_flag_needs_receiver_table(engine):
+    """seal(frame=True) without wg_ctx_set_receivers is refused (WG_EINVAL) before any launch,
+    and the host path refuses WG_F_FRAME instead of ignoring it."""
+    import torch
     W = wg()
-    assert W._lib.WG_F_FRAME == 2
+    dev = torch.device("cuda", 0)
+    engine.set_receivers(None)
+    d = torch.from_numpy(W.desc_as_int64(W.pack_desc([0], [16], [0], 10, 0))).to(dev)
+    buf = torch.zeros(64, dtype=torch.uint8, device=dev)
+    with pytest.raises(W.WgError) as e:
+        engine.seal(d, buf, buf, 10, frame=True)
+    assert e.value.code == W._lib.WG_EINVAL
+    lib = W.lib()
+    hd = W.pack_desc([0], [16], [0], 10, 0)
+    hb = np.zeros(64, np.uint8)
+    assert lib.wg_seal_host(engine.ctx, hd.ctypes.data, 1, hb.ctypes.data, 64, hb.ctypes.data, 64, 10,
+                            W._lib.WG_F_FRAME) == W._lib.WG_EINVAL
+
+
+@pytest.mark.gpu
+def test_frame_flag_leaves_rejected_packets_untouched(engine):
+    """A packet the seal skips (len > max_len, input or output range outside its buffer,
+    key slot past the table) gets no header either: its 16 header bytes keep their value."""
+    import torch
+    W = wg()
+    dev = torch.device("cuda", 0)
+    n, slot, L = 6, 256, 100
+    keys = splitmix_np(931, 32)
+    tun = splitmix_np(932, n * 128)
+    desc = np.zeros(n, O.WG_PKT)
+    desc["in_off"] = np.arange(n, dtype=np.uint64) * 128
+    desc["out_off"] = np.arange(n, dtype=np.uint64) * slot + 16
+    desc["counter"] = np.arange(n, dtype=np.uint64) + 5
+    desc["len"] = L
+    desc["len"][1] = 120                   # > max_len
+    desc["in_off"][2] = tun.size - 50      # input runs past the end of `in`
+    desc["out_off"][3] = n * slot - 40     # ct||tag runs past the end of `out`
+    desc["key_slot"][4] = engine.key_slots  # no such key slot
+    receivers = np.arange(engine.key_slots, dtype=np.uint32) + 1000
+    engine.set_keys(0, keys.tobytes())
+    engine.set_receivers(torch.from_numpy(receivers.view(np.int32)).to(dev))
+    try:
+        ring = torch.full((n * slot,), 0xA5, dtype=torch.uint8, device=dev)
+        engine.seal(torch.from_numpy(W.desc_as_int64(desc)).to(dev), torch.from_numpy(tun).to(dev), ring, L,
+                    frame=True)
+        torch.cuda.synchronize()
+    finally:
+        engine.set_receivers(None)
+    got = ring.cpu().numpy()
+    ref = np.full(n * slot, 0xA5, np.uint8)
+    O.seal_batch(desc[[0, 5]].copy(), tun, ref, keys, threads=1)
+    O.frame_headers(desc, receivers, ref, key_slots=engine.key_slots, in_size=tun.size, max_len=L)
+    assert np.array_equal(got, ref)
+    for i in (1, 2, 3, 4):
+        o = int(desc["out_off"][i])
+        assert (got[o - 16:o] == 0xA5).all(), i
+
+
+@pytest.mark.gpu
+def test_receiver_table_is_validated(engine):
+    """wg_ctx_set_receivers refuses a table shorter than the key table or not in device memory."""
+    import torch
+    W = wg()
+    with pytest.raises(W.WgError):
+        engine.set_receivers(torch.zeros(engine.key_slots - 1, dtype=torch.int32, device="cuda"))
+    with pytest.raises(W.WgError):
+        engine.set_receivers(torch.zeros(engine.key_slots, dtype=torch.int32))  # host tensor
+    lib = W.lib()
+    host = np.zeros(engine.key_slots, np.uint32)
+    assert lib.wg_ctx_set_receivers(engine.ctx, host.ctypes.data, engine.key_slots) == W._lib.WG_EINVAL

@@ -1,0 +1,189 @@
+"""BASELINE configs at full size on the MI355X (pytest -m gpu), every compared byte against
+the oracle (oracle/liboracle.so), plus the batch API's argument contract.
+
+  C2 = configs[2]: 65536 packets of 64..9000 B over 256 session keys, every packet compared
+  C3 = configs[3]: 8,388,608 x 1420 B sharded by session (dist.shard_packets), 1024 keys on
+       one GPU: full seal -> open round trip on the device, a seeded 65536-packet subset
+       compared byte for byte with the oracle
+"""
+import importlib
+
+import numpy as np
+import pytest
+
+from wgtest import oracle, splitmix_np, wg
+
+pytestmark = pytest.mark.gpu
+O = oracle()
+
+
+def _dev():
+    import torch
+    assert torch.cuda.is_available()
+    return torch, torch.device("cuda", 0)
+
+
+def test_c2_full_every_packet(engine):
+    torch, dev = _dev()
+    W = wg()
+    n = 65536
+    lengths = (64 + splitmix_np(0x5EED2026, 4 * n).view("<u4") % (9000 - 64 + 1)).astype(np.int64)
+    S = ((lengths + 16 + 15) // 16) * 16
+    off = np.concatenate([[0], np.cumsum(S)[:-1]]).astype(np.uint64)
+    total = int(S.sum())
+    desc = W.pack_desc(off, off, np.arange(n, dtype=np.uint64) // 256, lengths, np.arange(n) % 256)
+    keys = splitmix_np(0xC0FFEE, 32 * 256)
+    pt = splitmix_np(0x5EED2027, total)
+    engine.set_keys(0, keys.tobytes())
+    d = torch.from_numpy(W.desc_as_int64(desc)).to(dev)
+    dpt = torch.from_numpy(pt).to(dev)
+    dct = torch.zeros(total, dtype=torch.uint8, device=dev)
+    engine.seal(d, dpt, dct, 9000)
+    torch.cuda.synchronize()
+    ref = np.zeros(total, np.uint8)
+    O.seal_batch(desc, pt, ref, keys, threads=16)
+    got = dct.cpu().numpy()
+    assert np.array_equal(got, ref)  # every packet's ct || tag (and untouched slack)
+    # open every packet, 1% tampered
+    bad = np.nonzero(splitmix_np(99, n) < 3)[0]
+    for i in bad:
+        got[int(off[i]) + int(lengths[i])] ^= 0x10
+    back = torch.zeros(total, dtype=torch.uint8, device=dev)
+    st = torch.full((n,), 7, dtype=torch.int32, device=dev)
+    engine.open(d, torch.from_numpy(got).to(dev), back, st, 9000)
+    torch.cuda.synchronize()
+    exp = np.zeros(n, np.int32)
+    exp[bad] = 1
+    assert np.array_equal(st.cpu().numpy(), exp)
+    b = back.cpu().numpy()
+    want = pt.copy()
+    bad_set = set(bad.tolist())
+    for i in range(n):
+        o, L = int(off[i]), int(lengths[i])
+        want[o + L:o + int(S[i])] = 0  # slack between packets: never written
+        if i in bad_set:
+            want[o:o + L] = 0  # unauthenticated plaintext scrubbed
+    assert np.array_equal(b, want)
+
+
+def test_c3_sharded_roundtrip_and_oracle_subset():
+    """configs[3] on one GPU: 8M x 1420 B, session s -> rank s mod world (world 1 here),
+    each session counting its packets from 0; 1024 keys."""
+    torch, dev = _dev()
+    W = wg()
+    D = importlib.import_module("wireguard-java_amd.dist")
+    total, L, sessions, stride = 8 * 1024 * 1024, 1420, 1024, 1440
+    slots, _, counters = D.shard_packets(total, sessions, 0, 1)
+    n = len(slots)
+    assert n == total
+    off = np.arange(n, dtype=np.uint64) * stride
+    desc = W.pack_desc(off, off, counters, L, slots)
+    keys = splitmix_np(0xC3C3, 32 * sessions)
+    eng = W.Engine(0, key_slots=sessions)
+    try:
+        eng.set_keys(0, keys.tobytes())
+        d = torch.from_numpy(W.desc_as_int64(desc)).to(dev)
+        g = torch.Generator(device=dev)
+        g.manual_seed(1234)
+        pt = torch.randint(0, 256, (n * stride,), dtype=torch.uint8, device=dev, generator=g)
+        ct = torch.zeros_like(pt)
+        eng.seal(d, pt, ct, L, uniform=True)
+        back = torch.zeros_like(pt)
+        st = torch.full((n,), 7, dtype=torch.int32, device=dev)
+        eng.open(d, ct, back, st, L, uniform=True)
+        torch.cuda.synchronize()
+        assert int(st.abs().sum().item()) == 0
+        assert torch.equal(back.view(n, stride)[:, :L], pt.view(n, stride)[:, :L])
+        # seeded 65536-packet subset, every byte of ct || tag against the oracle
+        pick = np.sort(np.random.default_rng(33).choice(n, 65536, replace=False))
+        idx = torch.from_numpy(pick.astype(np.int64)).to(dev)
+        sub_pt = pt.view(n, stride).index_select(0, idx).cpu().numpy()
+        sub_ct = ct.view(n, stride).index_select(0, idx).cpu().numpy()
+        sd = desc[pick].copy()
+        sd["in_off"] = sd["out_off"] = np.arange(len(pick), dtype=np.uint64) * stride
+        ref = np.zeros(len(pick) * stride, np.uint8)
+        O.seal_batch(sd, sub_pt.reshape(-1), ref, keys, threads=16)
+        ref = ref.reshape(len(pick), stride)
+        assert np.array_equal(sub_ct[:, :L + 16], ref[:, :L + 16])
+        del pt, ct, back
+    finally:
+        eng.close()
+
+
+def test_in_place_open_bad_tag_zero_fills(engine):
+    """Batch open with in == out (the incoming buffer holds ct, pt is written over it):
+    a good packet decrypts in place; a forged one comes back WG_PKT_BADTAG with its
+    plaintext range zero-filled. The reference leaves the ciphertext of a forged packet in
+    place (ChaCha20Poly1305.java:51-53 throws before decrypting); the batch API documents the
+    zero-fill instead (include/wgaead.h), and the per-packet wg_open1 keeps
+    dst untouched."""
+    torch, dev = _dev()
+    W = wg()
+    n, L, S = 4, 300, 320
+    off = np.arange(n, dtype=np.uint64) * (S + 16)
+    desc = W.pack_desc(off, off, np.arange(n, dtype=np.uint64), L, 0)
+    keys = splitmix_np(61, 32)
+    pt = splitmix_np(62, n * (S + 16))
+    sealed = np.zeros_like(pt)
+    O.seal_batch(desc, pt, sealed, keys, threads=1)
+    sealed[int(off[2]) + L] ^= 1  # forge packet 2's tag
+    engine.set_keys(0, keys.tobytes())
+    buf = torch.from_numpy(sealed.copy()).to(dev)
+    st = torch.zeros(n, dtype=torch.int32, device=dev)
+    engine.open(torch.from_numpy(W.desc_as_int64(desc)).to(dev), buf, buf, st, L, uniform=True)
+    torch.cuda.synchronize()
+    assert st.cpu().tolist() == [0, 0, 1, 0]
+    got = buf.cpu().numpy()
+    for i in range(n):
+        o = int(off[i])
+        want = np.zeros(L, np.uint8) if i == 2 else pt[o:o + L]
+        assert np.array_equal(got[o:o + L], want), i
+        assert np.array_equal(got[o + L:o + L + 16], sealed[o + L:o + L + 16])  # tags untouched
+
+
+def test_batch_argument_contract(engine):
+    """open needs a status array; unknown flag bits and WG_F_FRAME on open are
+    refused (WG_EINVAL) instead of silently ignored."""
+    torch, dev = _dev()
+    W = wg()
+    lib = W.lib()
+    d = torch.from_numpy(W.desc_as_int64(W.pack_desc([0], [0], [0], 16, 0))).to(dev)
+    b = torch.zeros(64, dtype=torch.uint8, device=dev)
+    s = torch.zeros(1, dtype=torch.int32, device=dev)
+    E = W._lib.WG_EINVAL
+    assert lib.wg_open_batch(engine.ctx, d.data_ptr(), 1, b.data_ptr(), 64, b.data_ptr(), 64, None, 16, 0, None) == E
+    assert lib.wg_open_batch(engine.ctx, d.data_ptr(), 1, b.data_ptr(), 64, b.data_ptr(), 64, s.data_ptr(), 16,
+                             W._lib.WG_F_FRAME, None) == E
+    assert lib.wg_seal_batch(engine.ctx, d.data_ptr(), 1, b.data_ptr(), 64, b.data_ptr(), 64, 16, 0x80, None) == E
+    assert lib.wg_open_batch(engine.ctx, d.data_ptr(), 0, b.data_ptr(), 64, b.data_ptr(), 64, None, 16, 0, None) == 0
+
+
+def test_mixed_batch_on_two_streams_shares_plan_workspace(engine):
+    """Two mixed-length (longest-first ordered) batches enqueued on two different streams of
+    one context: the second waits for the first's plan workspace, both bit-exact."""
+    torch, dev = _dev()
+    W = wg()
+    outs = []
+    refs = []
+    s1, s2 = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    keys = splitmix_np(71, 32 * 4)
+    engine.set_keys(0, keys.tobytes())
+    for k, stream in enumerate((s1, s2)):
+        n = 40000 + 5000 * k  # more packets than resident slots: the LPT order is used
+        lengths = (splitmix_np(72 + k, 4 * n).view("<u4") % 1500).astype(np.int64)
+        S = ((lengths + 16 + 15) // 16) * 16
+        off = np.concatenate([[0], np.cumsum(S)[:-1]]).astype(np.uint64)
+        desc = W.pack_desc(off, off, np.arange(n, dtype=np.uint64), lengths, np.arange(n) % 4)
+        pt = splitmix_np(80 + k, int(S.sum()))
+        ref = np.zeros_like(pt)
+        O.seal_batch(desc, pt, ref, keys, threads=16)
+        d = torch.from_numpy(W.desc_as_int64(desc)).to(dev)
+        dp = torch.from_numpy(pt).to(dev)
+        out = torch.zeros_like(dp)
+        torch.cuda.synchronize()
+        engine.seal(d, dp, out, int(lengths.max()), stream=stream.cuda_stream)
+        outs.append((out, d, dp))
+        refs.append(ref)
+    torch.cuda.synchronize()
+    for (out, _, _), ref in zip(outs, refs):
+        assert np.array_equal(out.cpu().numpy(), ref)

@@ -8,12 +8,12 @@ import sys
 for d in sys.argv[1:]:
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     dur = collections.defaultdict(list)
-    for f in sorted(glob.glob(f"gpurun_out/{d}/p*/**/*counter_collection.csv", recursive=True)):
+    for f in sorted(glob.glob(f"gpurun_out/{d}/**/*counter_collection.csv", recursive=True)):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
-            if "wgk::" not in k:
+            if "k_transport" not in k and "k_wave" not in k and "k_tile" not in k:
                 continue
-            k = k.split("(")[0].replace("void wgk::", "")
+            k = f.split("/")[-3] + ":" + k.split("(")[0].replace("void ", "")
             acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
             if r["Counter_Name"] == "SQ_WAVES":
                 dur[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))

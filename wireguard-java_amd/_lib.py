@@ -38,7 +38,7 @@ _ERRNAMES = {WG_EINVAL: "EINVAL", WG_ENOMEM: "ENOMEM", WG_ERANGE: "ERANGE", WG_E
 
 class WgError(RuntimeError):
     """A negative return code of libwgaead (mirrors the RuntimeException the reference's
-    FFM wrappers raise on a failed downcall, ChaCha20.java:293-295)."""
+    FFM wrappers raise on a failed downcall, ChaCha20.java:102,110,141)."""
 
     def __init__(self, code: int, msg: str = ""):
         super().__init__(f"libwgaead {_ERRNAMES.get(code, code)}: {msg}")
@@ -75,12 +75,14 @@ SIGNATURES = [
     ("wg_keys_zero", _I, [_VP, _U32, _U32]),
     ("wg_seal_batch", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _U32, _U32, _VP]),
     ("wg_open_batch", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _VP, _U32, _U32, _VP]),
-    ("wg_ctx_set_receivers", _I, [_VP, _VP]),
-    ("wg_frame_seal", _I, [_VP, _VP, _U32, _VP, _VP, _U64, _VP]),
+    ("wg_ctx_set_receivers", _I, [_VP, _VP, _U32]),
+    ("wg_frame_seal", _I, [_VP, _VP, _U32, _VP, _VP, _U64, _U64, _U32, _VP]),
     ("wg_parse_open", _I, [_VP, _VP, _U64, _VP, _VP, _VP, _U32, _VP, _VP, _VP]),
     ("wg_aead_batch", _I, [_VP, _I, _VP, _U32, _VP, _U64, _VP, _U64, _VP, _U64, _VP, _U32, _VP]),
     ("wg_seal1", _I, [_VP, _U32, _U64, _VP, _U32, _VP]),
     ("wg_open1", _I, [_VP, _U32, _U64, _VP, _U32, _VP]),
+    ("wg_batcher_config", _I, [_VP, _U32, _U32]),
+    ("wg_batcher_stats", _I, [_VP, ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
     ("wg_seal_host", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _U32, _U32]),
     ("wg_open_host", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _VP, _U32, _U32]),
     ("wg_host_alloc", _I, [_VP, _U64, ctypes.POINTER(_VP)]),

@@ -3,7 +3,7 @@
 // ChaCha20 block (RFC 8439 2.3) restated for 64-wide CDNA4 waves: one lane owns
 // one 64-byte counter block in 16 VGPRs. Reference semantics:
 //   chacha_permute / chacha_block_generic  ax.xz.wireguard.noise/src/main/c/chacha-generic.c:10-78
-//   state layout (constants, key, ctr, nonce) ChaCha20.java:247-266
+//   state layout (constants, key, ctr, nonce) ChaCha20.java:55-74
 // Poly1305 (RFC 8439 2.5) in radix 2^26 (5 limbs in VGPRs) with v_mad_u64_u32
 // products; canonical final reduction as poly1305-donna-64.h:154-223.
 //

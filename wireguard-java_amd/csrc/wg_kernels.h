@@ -31,7 +31,6 @@ struct TileParams {
   const uint32_t* ntiles_dev;  // non-uniform: tile count computed on device
   uint32_t max_tile_pkts;      // LDS sizing of the per-packet records
   uint32_t poly_g;             // lanes per packet in the Poly1305 phase
-  uint64_t* stamps;            // diagnostic build only (WG_DIAG): per-tile phase timestamps
 };
 
 template <int MODE, bool GENERAL>

@@ -1,0 +1,566 @@
+// wg_transport.hip — the transport-data seal/open kernel for gfx950 (product path).
+//
+// Replaces the per-packet SymmetricKeypair.cipher / decipher
+// (ax.xz.wireguard.noise/src/main/java/ax/xz/wireguard/noise/handshake/SymmetricKeypair.java:63-83)
+// over a batch of independent packets: ChaCha20 keystream from counter 1, Poly1305 key from
+// block 0, MAC over ct || pad16 || le64(0) || le64(len) (ChaCha20Poly1305.java:31-93), with the
+// reference's nonce LE64(counter) || 0^4 (SymmetricKeypair.java:52-61).
+//
+// Layout (k_transport<MODE>): a wave is 8 SLOTS of 8 lanes; a slot owns one packet at a
+// time and streams it in ROUNDS of 8 ChaCha20 counter blocks (512 bytes):
+//   * lane j of the slot computes block b = 8 round + j in registers (block 0 = the
+//     Poly1305 one-time key), XORs its 64 payload bytes, stores them, and leaves the
+//     round's MAC input (the ciphertext) in a 4 KB per-wave LDS image;
+//   * the same 8 lanes advance an 8-strided Horner evaluation of the MAC polynomial
+//     over the image (lane j owns positions = j mod 8, multiplier r^8, front padding
+//     so the length block lands on lane 7); on the last round lane j scales its partial
+//     by r^(8-j), the slot sums the 8 partials and lane 0 finishes the tag.
+// Slots are persistent: slot g of S processes batch positions g, 2S-1-g, 2S+g, ... (a
+// snake over the grid). Mixed-length batches are first ordered longest-first on the
+// device (k_lpt_*), so the snake deals every slot one long and one short packet
+// (LPT); uniform batches take positions in order. The next packet's descriptor is
+// prefetched one packet ahead (one dword per lane), so a slot never waits on a
+// dependent descriptor load when it starts a packet.
+//
+// IO: 16-byte aligned packets move as dwordx4 (a tail block reads whole 16-B chunks,
+// which never leave the granule of a valid byte, and masks); other alignments read
+// aligned dwords and realign with v_alignbyte, and store through a per-lane LDS stage.
+// Open writes the plaintext in the same pass and zero-fills it again if the tag does
+// not verify (the host per-packet wrappers copy back only verified plaintext, as
+// ChaCha20Poly1305.java:40-56 leaves dst untouched).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "wg_device.h"
+#include "wg_kernels.h"
+
+namespace wgt {
+
+using namespace wgd;
+
+#ifndef WG_TW
+#define WG_TW 4
+#endif
+constexpr uint32_t TW = WG_TW;      // waves per workgroup
+constexpr uint32_t LPT_BINS = 130;  // round counts 0..129 (65535-B payload = 1025 blocks = 129 rounds)
+
+struct TransportParams {
+  const wg_pkt* desc;
+  const uint32_t* order;  // batch position -> packet index (longest first); nullptr = identity
+  uint32_t n;
+  uint32_t slots;         // S = 8 x waves in the grid
+  uint32_t max_len;
+  uint32_t key_slots;
+  const uint8_t* in;
+  uint64_t in_size;
+  uint8_t* out;
+  uint64_t out_size;
+  const uint32_t* keys;   // device key table, 8 words per slot
+  uint32_t* status;       // open: per-packet WG_PKT_*
+};
+
+// ---- lane exchange inside an 8-lane slot -------------------------------------------
+// ds_swizzle bitmask mode inside each 32-lane half: src = ((lane & and) | or) ^ xor.
+template <int K>
+__device__ __forceinline__ uint32_t bcast8(uint32_t v) {  // every lane of the slot reads lane K of it
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (K << 5));
+}
+template <int X>
+__device__ __forceinline__ uint32_t xor8(uint32_t v) {  // lane reads lane ^ X (X < 8)
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1f | (X << 10));
+}
+
+// ---- validity of one transport descriptor (shared by seal, open and the framing) ----
+template <int MODE>
+__device__ __forceinline__ bool transport_valid(uint64_t in_off, uint64_t out_off, uint32_t len, uint32_t ks,
+                                                uint32_t max_len, uint32_t key_slots, uint64_t in_size,
+                                                uint64_t out_size) {
+  const uint64_t in_need = (uint64_t)len + (MODE == WG_MODE_OPEN ? 16u : 0u);
+  const uint64_t out_need = (uint64_t)len + (MODE == WG_MODE_SEAL ? 16u : 0u);
+  return len <= max_len && ks < key_slots && in_off <= in_size && in_need <= in_size - in_off &&
+         out_off <= out_size && out_need <= out_size - out_off;
+}
+
+// 16 bytes at p (any alignment), `avail` (1..16) of them inside the packet: the aligned dwords
+// covering them (none leaves the granule of a valid byte), realigned with v_alignbyte
+__device__ __forceinline__ uint4 chunk_any(const uint8_t* p, uint32_t avail) {
+  const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
+  const uint32_t* q = (const uint32_t*)(p - sh);
+  const uint32_t nw = (sh + avail + 3u) >> 2;
+  uint32_t W[5];
+#pragma unroll
+  for (uint32_t k = 0; k < 5; ++k) W[k] = k < nw ? q[k] : 0u;
+  return make_uint4(__builtin_amdgcn_alignbyte(W[1], W[0], sh), __builtin_amdgcn_alignbyte(W[2], W[1], sh),
+                    __builtin_amdgcn_alignbyte(W[3], W[2], sh), __builtin_amdgcn_alignbyte(W[4], W[3], sh));
+}
+
+// bytes >= cb (1..15) of a 16-B chunk zeroed: dword k keeps clamp(8 cb - 32 k, 0, 32) low bits
+__device__ __forceinline__ uint4 mask_chunk(uint4 v, uint32_t cb) {
+  int c8 = (int)(8u * cb);
+  asm volatile("" : "+v"(c8));  // keep the mask arithmetic in the (rare) partial-chunk path
+  uint32_t t[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t[k] &= ~(uint32_t)(~0ull << min(max(c8 - 32 * k, 0), 32));
+  return make_uint4(t[0], t[1], t[2], t[3]);
+}
+
+// cb (1..16) bytes of a chunk to p: oal bit 2 = p 16-B aligned, bit 3 = p 4-B aligned
+__device__ __forceinline__ void store_chunk(uint8_t* p, uint32_t cb, uint4 o, uint32_t oal) {
+  if (cb == 16u && (oal & 4u)) {
+    *(uint4*)p = o;
+    return;
+  }
+  const uint32_t t[4] = {o.x, o.y, o.z, o.w};
+  if (oal & 8u) {
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; ++k) {
+      const int r = (int)cb - 4 * (int)k;
+      if (r >= 4) {
+        ((uint32_t*)p)[k] = t[k];
+      } else if (r > 0) {
+        uint8_t* q = p + 4u * k;
+        q[0] = (uint8_t)t[k];
+        if (r > 1) q[1] = (uint8_t)(t[k] >> 8);
+        if (r > 2) q[2] = (uint8_t)(t[k] >> 16);
+      }
+    }
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i < 16u; ++i)
+      if (i < cb) p[i] = (uint8_t)(t[i >> 2] >> (8u * (i & 3u)));
+  }
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void gbl_cvoid;
+
+__device__ __forceinline__ uint32_t load_u32_any(const uint8_t* p) {
+  if ((((uintptr_t)p) & 3u) == 0) return *(const uint32_t*)p;
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+__device__ __forceinline__ void store_u32_any(uint8_t* p, uint32_t v) {
+  if ((((uintptr_t)p) & 3u) == 0) {
+    *(uint32_t*)p = v;
+    return;
+  }
+  p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
+}
+
+// orders this wave's LDS writes before its other lanes' reads
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ uint32_t batch_pos(uint32_t g, uint32_t k, uint32_t S) {
+  return k * S + ((k & 1u) ? S - 1u - g : g);
+}
+
+// ---- the kernel ------------------------------------------------------------------------
+// Register budget: <= 64 VGPRs, so 8 waves share a SIMD (the payload stream and the ARX
+// rounds of other waves hide each other's latency). What is constant for a packet lives
+// in a 128-B LDS record per slot and is re-read where it is used; lane-derived values are
+// recomputed from an opaque copy of the lane id instead of being held across the rounds.
+struct SlotRec {  // per slot, in LDS
+  uint4 addr;     // {in_off lo, in_off hi, out_off lo, out_off hi} (pointers are rebuilt from the kernel
+                  // arguments, so the compiler keeps global, not flat, memory instructions)
+  uint4 meta;     // {ctr lo, ctr hi, len, flags}: bit 0 valid, bit 1 input / bit 2 output 16-B aligned,
+                  // bit 3 output 4-B aligned
+  uint4 R0;       // R = r^8 limbs 0..3
+  uint4 R1;       // {R4, 5 R1, 5 R2, 5 R3}
+  uint4 R2;       // {5 R4, -, -, -}
+  uint4 s;        // Poly1305 s
+  uint4 key[2];   // ChaCha20 key
+};
+static_assert(sizeof(SlotRec) == 128, "slot record is 128 B");
+
+__device__ __forceinline__ uint32_t opaque_lane() {
+  uint32_t x = threadIdx.x & 63u;
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8))) k_transport(TransportParams P) {
+  static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
+  __shared__ uint4 img_[TW][4 * 64];     // 4 KB per wave: [chunk q][lane] = the round's payload / MAC input
+  __shared__ SlotRec rec_[TW][8];        // 1 KB per wave
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint4* const img = img_[wv];
+  SlotRec* const rec = rec_[wv];
+  const uint32_t S = P.slots;
+  const uint32_t g = (blockIdx.x * TW + wv) * 8u + (opaque_lane() >> 3);
+
+  // descriptor prefetch: dword j of the next packet's wg_pkt (32 B = 8 dwords, one per lane)
+  uint32_t gen = 0;
+  uint32_t nxt;
+  {
+    const uint32_t pos = batch_pos(g, 0, S);
+    nxt = pos < P.n ? (P.order ? P.order[pos] : pos) : ~0u;
+  }
+  uint32_t dnext = nxt != ~0u ? ((const uint32_t*)(P.desc + nxt))[opaque_lane() & 7u] : 0u;
+
+  bool have = false;
+  uint32_t pkt = 0, round = 0;
+  uint32_t acc[5], W[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) acc[i] = W[i] = 0;
+
+  while (true) {
+    // ---- slots without a packet take their next one ------------------------------------
+    if (!have && nxt != ~0u) {
+      const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
+      pkt = nxt;
+      const uint32_t d0 = bcast8<0>(dnext), d1 = bcast8<1>(dnext), d2 = bcast8<2>(dnext), d3 = bcast8<3>(dnext);
+      const uint32_t len = bcast8<6>(dnext), ks = bcast8<7>(dnext);
+      const uint64_t in_off = (uint64_t)d0 | ((uint64_t)d1 << 32);
+      const uint64_t out_off = (uint64_t)d2 | ((uint64_t)d3 << 32);
+      const bool valid =
+          transport_valid<MODE>(in_off, out_off, len, ks, P.max_len, P.key_slots, P.in_size, P.out_size);
+      const uintptr_t ia = (uintptr_t)(P.in + in_off), oa = (uintptr_t)(P.out + out_off);
+      const uint32_t al = ((ia & 15u) == 0 ? 2u : 0u) | ((oa & 15u) == 0 ? 4u : 0u) | ((oa & 3u) == 0 ? 8u : 0u);
+      if (valid) ((uint32_t*)rec[s].key)[j] = P.keys[8u * ks + j];
+      const uint32_t c0 = bcast8<4>(dnext), c1 = bcast8<5>(dnext);  // all 8 lanes active: swizzles read live lanes
+      if (j == 0) {
+        rec[s].addr = make_uint4(d0, d1, d2, d3);
+        rec[s].meta = make_uint4(c0, c1, len, (valid ? 1u : 0u) | al);
+      }
+      round = 0;
+      have = true;
+      // prefetch the descriptor of the slot's following packet
+      ++gen;
+      const uint32_t pos = batch_pos(g, gen, S);
+      nxt = pos < P.n ? (P.order ? P.order[pos] : pos) : ~0u;
+      dnext = nxt != ~0u ? ((const uint32_t*)(P.desc + nxt))[j] : 0u;
+    }
+    if (!__any(have)) break;
+    wave_lds_sync();  // the slot records before the lanes read them
+
+    uint32_t x[16];
+    {
+      // ---- payload prefetch: LDS-DMA straight into this lane's slice of the image ---------
+      // (no registers held across the ARX rounds; unaligned packets load after them)
+      const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
+      const uint4 meta = rec[s].meta;
+      const uint32_t len = meta.z;
+      const uint32_t nb = (meta.w & 1u) ? ((len + 63u) >> 6) + 1u : 0u;
+      const uint32_t b = 8u * round + j;
+      if (have && b < nb && b > 0u) {
+        const uint32_t off = 64u * (b - 1u);
+        const uint32_t nbytes = min(64u, len - off);
+        const uint4 ad = rec[s].addr;
+        const uint8_t* src = P.in + (((uint64_t)ad.x | ((uint64_t)ad.y << 32)) + off);
+        if (meta.w & 2u) {
+          // chunks holding a valid byte, each read whole (an aligned 16-B read stays in the granule
+          // of its first byte); lane i's chunk q lands at img[q * 64 + i]
+          __builtin_amdgcn_global_load_lds((gbl_cvoid*)src, (lds_void*)&img[0], 16, 0, 0);
+          if (nbytes > 16u) __builtin_amdgcn_global_load_lds((gbl_cvoid*)(src + 16), (lds_void*)&img[64], 16, 0, 0);
+          if (nbytes > 32u) __builtin_amdgcn_global_load_lds((gbl_cvoid*)(src + 32), (lds_void*)&img[128], 16, 0, 0);
+          if (nbytes > 48u) __builtin_amdgcn_global_load_lds((gbl_cvoid*)(src + 48), (lds_void*)&img[192], 16, 0, 0);
+        } else {  // unaligned input: the same image, staged through registers one chunk at a time
+#pragma unroll
+          for (uint32_t q = 0; q < 4u; ++q)
+            if (16u * q < nbytes) img[64u * q + lane] = chunk_any(src + 16u * q, min(16u, nbytes - 16u * q));
+        }
+      }
+      // ---- ChaCha20: block b = 8 round + j ----------------------------------------------
+      chacha20_block_lds(rec[s].key, b, meta.x, meta.y, 0u, x);  // every lane (SIMT); act lanes use it
+    }
+
+    if (__any(have && round == 0)) {  // round 0: lane 0 of the slot holds the one-time key r || s
+      const uint32_t lane = opaque_lane(), s = lane >> 3;
+      if (have && round == 0 && (lane & 7u) == 0) {
+        rec[s].R0 = make_uint4(x[0], x[1], x[2], x[3]);  // raw r, replaced by R = r^8 below
+        rec[s].s = make_uint4(x[4], x[5], x[6], x[7]);
+      }
+    }
+
+    // ---- XOR, store, MAC input into the image, one 16-B chunk at a time ----------------------
+    {
+      const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
+      const uint4 meta = rec[s].meta;
+      const uint32_t len = meta.z;
+      const uint32_t nb = (meta.w & 1u) ? ((len + 63u) >> 6) + 1u : 0u;
+      const uint32_t b = 8u * round + j;
+      if (have && b < nb && b > 0u) {
+        const uint32_t off = 64u * (b - 1u);
+        const uint32_t nbytes = min(64u, len - off);
+        const uint4 ad = rec[s].addr;
+        uint8_t* dst = P.out + (((uint64_t)ad.z | ((uint64_t)ad.w << 32)) + off);
+        const uint32_t oal = meta.w & 12u;  // bit 2: 16-B aligned output, bit 3: 4-B aligned
+        // the payload DMA (and the staged loads) must have landed in LDS: the compiler does not
+        // always see the LDS-DMA -> ds_read dependence, so wait for it explicitly
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (uint32_t q = 0; q < 4u; ++q) {
+          if (16u * q < nbytes) {
+            const uint32_t cb = min(16u, nbytes - 16u * q);  // valid bytes in this chunk
+            uint4 v = img[64u * q + lane];  // payload (the compiler waits for the DMA before this read)
+            if (cb < 16u) v = mask_chunk(v, cb);
+            if constexpr (MODE == WG_MODE_OPEN) {
+              if (cb < 16u) img[64u * q + lane] = v;  // the MAC input is the zero-padded ciphertext
+            }
+            uint4 o = make_uint4(x[4 * q] ^ v.x, x[4 * q + 1] ^ v.y, x[4 * q + 2] ^ v.z, x[4 * q + 3] ^ v.w);
+            if constexpr (MODE == WG_MODE_SEAL) {
+              if (cb < 16u) o = mask_chunk(o, cb);
+              img[64u * q + lane] = o;  // the MAC input is the ciphertext
+            }
+            store_chunk(dst + 16u * q, cb, o, oal);
+          }
+        }
+      }
+    }
+    wave_lds_sync();
+
+    // ---- round 0: r^1..r^8 (lane j gets r^(j+1)), R = r^8, W = r^(8-j) --------------------
+    // (after the XOR phase, so the 32 registers of keystream and payload are free again)
+    if (__any(have && round == 0)) {
+      if (have && round == 0) {
+        const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
+        const uint4 rr = rec[s].R0;
+        uint32_t y[5];
+        poly_r_limbs(rr.x, rr.y, rr.z, rr.w, y);
+#pragma unroll
+        for (uint32_t st = 1; st < 8u; st <<= 1) {
+          uint32_t z[5], zs[5];
+#pragma unroll
+          for (int i = 0; i < 5; ++i) z[i] = __shfl(y[i], (int)(j >= st ? lane - st : lane), 64);
+          poly_scale5(z, zs);
+          if (j >= st) poly_mul(y, z, zs);
+        }
+        uint32_t R[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+          R[i] = bcast8<7>(y[i]);
+          W[i] = xor8<7>(y[i]);
+          acc[i] = 0;
+        }
+        if (j == 0) {
+          rec[s].R0 = make_uint4(R[0], R[1], R[2], R[3]);
+          rec[s].R1 = make_uint4(R[4], 5u * R[1], 5u * R[2], 5u * R[3]);
+          rec[s].R2 = make_uint4(5u * R[4], 0u, 0u, 0u);
+        }
+      }
+      wave_lds_sync();
+    }
+
+    // ---- Poly1305 over this round's chunks -------------------------------------------------
+    if (have) {
+      const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
+      const uint4 meta = rec[s].meta;
+      if (meta.w & 1u) {
+        const uint32_t len = meta.z, nc = (len + 15u) >> 4;
+        const uint32_t M = nc + 1u, D = 8u * ((M + 7u) >> 3) - M;
+        const uint32_t c_lo = round ? 32u * round - 4u : 0u;
+        const uint32_t c_end = min(nc, 32u * round + 28u);
+        const uint32_t c0 = c_lo + ((j - ((c_lo + D) & 7u)) & 7u);
+        // chunk ci of the round sits in lane (ci >> 2) + 1 - 8 round of the slot, row ci & 3
+        const uint4* ip = &img[64u * (c0 & 3u) + (lane & ~7u) + ((c0 + 4u) >> 2) - 8u * round];
+        const uint4 q0 = rec[s].R0, q1 = rec[s].R1, q2 = rec[s].R2;
+        const uint32_t R[5] = {q0.x, q0.y, q0.z, q0.w, q1.x};
+        const uint32_t Rs[5] = {0u, q1.y, q1.z, q1.w, q2.x};
+#pragma unroll
+        for (uint32_t t = 0; t < 4u; ++t) {
+          if (c0 + 8u * t < c_end) {
+            const uint4 v = ip[2u * t];
+            poly_mul(acc, R, Rs);
+            uint32_t cl[5];
+            poly_block_limbs(v.x, v.y, v.z, v.w, 1u << 24, cl);
+#pragma unroll
+            for (int i = 0; i < 5; ++i) acc[i] += cl[i];
+          }
+        }
+      }
+    }
+
+    // ---- finish the packets whose last round this was ---------------------------------------
+    bool done;
+    {
+      const uint4 meta = rec[opaque_lane() >> 3].meta;
+      const uint32_t nb = (meta.w & 1u) ? ((meta.z + 63u) >> 6) + 1u : 0u;
+      done = have && 8u * (round + 1u) >= nb;  // invalid packets (nb = 0) finish at once
+    }
+    if (__any(done)) {
+      if (done) {  // slot-uniform: every lane of a finishing slot is here
+        const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
+        const uint4 meta = rec[s].meta;
+        const uint32_t len = meta.z;
+        const bool valid = meta.w & 1u;
+        if (valid) {
+          if (j == 7u) {  // the length block le64(0) || le64(len) is lane 7's last position
+            const uint4 q0 = rec[s].R0, q1 = rec[s].R1, q2 = rec[s].R2;
+            const uint32_t R[5] = {q0.x, q0.y, q0.z, q0.w, q1.x};
+            const uint32_t Rs[5] = {0u, q1.y, q1.z, q1.w, q2.x};
+            poly_mul(acc, R, Rs);
+            acc[2] += (len << 12) & M26;  // le64(len) at bit 64: limb 2 holds bits 52..77
+            acc[3] += len >> 14;
+            acc[4] += 1u << 24;
+          }
+          uint32_t Ws[5];
+          poly_scale5(W, Ws);
+          poly_mul(acc, W, Ws);
+        }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {  // slot sum (every lane of the slot ends with it)
+          acc[i] += xor8<1>(acc[i]);
+          acc[i] += xor8<2>(acc[i]);
+          acc[i] += xor8<4>(acc[i]);
+        }
+        const uint4 ad = rec[s].addr;
+        const uint8_t* inp = P.in + ((uint64_t)ad.x | ((uint64_t)ad.y << 32));
+        uint8_t* outp = P.out + ((uint64_t)ad.z | ((uint64_t)ad.w << 32));
+        uint32_t bad = valid ? 0u : 1u;
+        if (valid && j == 0) {
+          const uint4 sv = rec[s].s;
+          uint32_t tag[4];
+          poly_finish(acc, sv.x, sv.y, sv.z, sv.w, tag);
+          if constexpr (MODE == WG_MODE_SEAL) {
+            uint8_t* tp = outp + len;
+            if ((((uintptr_t)tp) & 15u) == 0) {
+              *(uint4*)tp = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+            } else {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) store_u32_any(tp + 4 * i, tag[i]);
+            }
+          } else {  // all 16 bytes compared, no early exit
+            const uint8_t* tp = inp + len;
+            uint32_t diff = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) diff |= load_u32_any(tp + 4 * i) ^ tag[i];
+            bad = diff ? 1u : 0u;
+          }
+        }
+        if constexpr (MODE == WG_MODE_OPEN) {
+          bad = bcast8<0>(bad);
+          if (j == 0 && P.status) P.status[pkt] = bad ? WG_PKT_BADTAG : WG_PKT_OK;
+          if (bad && valid) {  // scrub the unauthenticated plaintext written by this launch
+            for (uint32_t i = j; i < len; i += 8u) outp[i] = 0;
+          }
+        }
+        have = false;
+      }
+    }
+    if (have) ++round;
+    wave_lds_sync();  // this round's image and records before the next round rewrites them
+  }
+}
+
+// ---- longest-first order for mixed-length batches (LPT) ----------------------------------
+// key = rounds of the packet (invalid lengths sort last); counting sort into descending keys.
+template <int MODE>
+__device__ __forceinline__ uint32_t lpt_key(const wg_pkt* d, uint32_t i, uint32_t max_len) {
+  const uint32_t len = d[i].len;
+  if (len > max_len) return 0u;
+  const uint32_t nb = ((len + 63u) >> 6) + 1u;
+  return (nb + 7u) >> 3;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256) k_lpt_hist(const wg_pkt* d, uint32_t n, uint32_t max_len, uint32_t* hist) {
+  __shared__ uint32_t h[LPT_BINS];
+  for (uint32_t k = threadIdx.x; k < LPT_BINS; k += 256u) h[k] = 0;
+  __syncthreads();
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u)
+    atomicAdd(&h[lpt_key<MODE>(d, i, max_len)], 1u);
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < LPT_BINS; k += 256u)
+    if (h[k]) atomicAdd(&hist[k], h[k]);
+}
+
+// cursor[k] = number of packets with a larger key (one workgroup)
+__global__ void __launch_bounds__(256) k_lpt_offsets(const uint32_t* hist, uint32_t* cursor) {
+  __shared__ uint32_t h[LPT_BINS];
+  for (uint32_t k = threadIdx.x; k < LPT_BINS; k += 256u) h[k] = hist[k];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int k = (int)LPT_BINS - 1; k >= 0; --k) {
+      const uint32_t c = h[k];
+      h[k] = acc;
+      acc += c;
+    }
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < LPT_BINS; k += 256u) cursor[k] = h[k];
+}
+
+// order[pos] = packet: each workgroup reserves a range per key, then ranks its packets in it
+template <int MODE>
+__global__ void __launch_bounds__(256) k_lpt_scatter(const wg_pkt* d, uint32_t n, uint32_t max_len, uint32_t* cursor,
+                                                     uint32_t* order) {
+  __shared__ uint32_t cnt[LPT_BINS], base[LPT_BINS];
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  for (uint32_t k = threadIdx.x; k < LPT_BINS; k += 256u) cnt[k] = 0;
+  __syncthreads();
+  const uint32_t key = i < n ? lpt_key<MODE>(d, i, max_len) : 0u;
+  const uint32_t rank = i < n ? atomicAdd(&cnt[key], 1u) : 0u;
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < LPT_BINS; k += 256u)
+    if (cnt[k]) base[k] = atomicAdd(&cursor[k], cnt[k]);
+  __syncthreads();
+  if (i < n) order[base[key] + rank] = i;
+}
+
+// ---- wire framing (TransportPacket.java:18-35) --------------------------------------------
+// 16-B transport header {u8 4, u8 0[3], u32 receiver_index, u64 counter}, little-endian,
+// written with 4-B or 1-B stores by alignment.
+__device__ inline void put_header(uint8_t* h, uint32_t rx, uint64_t ctr) {
+  const uint32_t w[4] = {4u, rx, (uint32_t)ctr, (uint32_t)(ctr >> 32)};
+  if ((((uintptr_t)h) & 3u) == 0) {
+    uint32_t* h32 = (uint32_t*)h;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) h32[k] = w[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) h[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+  }
+}
+
+// One thread per packet: header of every packet the seal kernel accepted (the same
+// validity test), at out_off - 16 (UnencryptedOutgoingTransport.java:14-18 writes the
+// type and receiver index, EncryptedOutgoingTransport.java:11-14 the counter).
+__global__ void __launch_bounds__(256) k_frame_seal(const wg_pkt* __restrict__ d, uint32_t n,
+                                                    const uint32_t* __restrict__ rx, uint32_t max_len,
+                                                    uint32_t key_slots, uint64_t in_size,
+                                                    uint8_t* __restrict__ out, uint64_t out_size) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const wg_pkt p = d[i];
+  if (p.out_off < 16 ||
+      !transport_valid<WG_MODE_SEAL>(p.in_off, p.out_off, p.len, p.key_slot, max_len, key_slots, in_size, out_size))
+    return;
+  put_header(out + p.out_off - 16, rx[p.key_slot], p.counter);
+}
+
+// Open descriptors straight from received wire packets (UndecryptedIncomingTransport.java:20-33):
+// ciphertext at +16, plaintext right after the packet in the same buffer (:30).
+__global__ void __launch_bounds__(256) k_parse_open(const uint8_t* __restrict__ wire, uint64_t wire_size,
+                                                    const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
+                                                    const uint32_t* __restrict__ slot, uint32_t n,
+                                                    wg_pkt* __restrict__ d, uint32_t* __restrict__ st) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t o = off[i];
+  const uint32_t wl = len[i];
+  wg_pkt p;
+  p.in_off = o + 16;
+  p.out_off = o + wl;
+  p.key_slot = slot[i];
+  p.counter = 0;
+  p.len = WG_LEN_INVALID;
+  // packet [o, o+wl) plus its plaintext [o+wl, o+2wl-32) must lie inside the buffer
+  bool ok = wl >= 32 && o <= wire_size && (uint64_t)wl <= wire_size - o && (uint64_t)wl - 32 <= wire_size - o - wl;
+  if (ok) {
+    const uint8_t* h = wire + o;
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = load_u32_any(h + 4 * k);
+    ok = (w[0] & 0xffu) == 4u;  // only the type byte is checked (UndecryptedIncomingTransport.java:24-26)
+    if (ok) {
+      p.counter = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+      p.len = wl - 32;
+    }
+  }
+  d[i] = p;
+  if (st) st[i] = ok ? WG_PKT_OK : WG_PKT_BADHDR;
+}
+
+}  // namespace wgt

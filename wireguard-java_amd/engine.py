@@ -52,7 +52,7 @@ class Engine:
         self.ctx = ctx
         self.device = device
         self.key_slots = key_slots
-        self._free = list(range(key_slots - 1, -1, -1))
+        self._free = set(range(key_slots))
         self._slot_lock = threading.Lock()
         self._pinned = {}
 
@@ -71,9 +71,10 @@ class Engine:
         except Exception:
             pass
 
-    def set_kernel(self, name: str | None = "default", lanes: int = 2, variant: int = 0) -> None:
-        """Transport kernel for this engine's seal/open calls (wg_ctx_set_kernel); every
-        kernel computes the same bytes, only the speed differs."""
+    def set_kernel(self, name: str | None = "default", lanes: int = 0, variant: int = 0) -> None:
+        """Transport kernel for this engine's seal/open calls (wg_ctx_set_kernel): "default"
+        (k_transport), "wave1" (the round-1 kernel) or "tile"; every kernel computes the
+        same bytes, only the speed differs."""
         L.check(self._lib.wg_ctx_set_kernel(self.ctx, None if name is None else name.encode(), lanes, variant))
 
     @property
@@ -85,16 +86,27 @@ class Engine:
 
     # ---- keys (SymmetricKeypair.java:39-50, 85-93) ------------------------------
     def alloc_slots(self, n: int) -> list[int]:
+        """Claim n free key slots (lowest first). Callers upload each slot's key on its
+        own (set_keys(slot, key)): claimed slots need not be adjacent after frees."""
         with self._slot_lock:
             if len(self._free) < n:
                 raise L.WgError(L.WG_ERANGE, "key table full")
-            return [self._free.pop() for _ in range(n)]
+            got = sorted(self._free)[:n]
+            self._free.difference_update(got)
+            return got
 
     def free_slots(self, slots):
+        """Zero and release slots claimed with alloc_slots (SymmetricKeypair.clean). A slot
+        that is not currently claimed is an error, so a double release cannot hand one
+        slot to two keypairs."""
+        with self._slot_lock:
+            bad = [s for s in slots if s in self._free or not 0 <= s < self.key_slots]
+            if bad or len(set(slots)) != len(slots):
+                raise L.WgError(L.WG_EINVAL, f"key slots {slots} are not all claimed")
         for s in slots:
             self.zero_keys(s, 1)
         with self._slot_lock:
-            self._free.extend(slots)
+            self._free.update(slots)
 
     def set_keys(self, first_slot: int, keys) -> None:
         k = np.ascontiguousarray(np.frombuffer(bytes(keys), np.uint8) if not isinstance(keys, np.ndarray) else keys,
@@ -125,18 +137,30 @@ class Engine:
 
     def set_receivers(self, receivers) -> None:
         """wg_ctx_set_receivers: device tensor of receiver_index per key slot for
-        seal(..., frame=True); the tensor must stay alive while seals use it."""
+        seal(..., frame=True) — contiguous, 4-byte integers, on this engine's device, at
+        least key_slots entries; the engine keeps it alive while seals use it."""
+        if receivers is None:
+            L.check(self._lib.wg_ctx_set_receivers(self.ctx, None, 0))
+            self._receivers = None
+            return
+        if receivers.device.type != "cuda" or receivers.device.index not in (None, self.device):
+            raise L.WgError(L.WG_EINVAL, f"receiver table on {receivers.device}, engine on cuda:{self.device}")
+        if not receivers.is_contiguous() or receivers.element_size() != 4:
+            raise L.WgError(L.WG_EINVAL, "receiver table must be a contiguous int32/uint32 tensor")
+        if receivers.numel() < self.key_slots:
+            raise L.WgError(L.WG_ERANGE, f"receiver table has {receivers.numel()} entries for {self.key_slots} slots")
+        L.check(self._lib.wg_ctx_set_receivers(self.ctx, receivers.data_ptr(), receivers.numel()))
         self._receivers = receivers
-        L.check(self._lib.wg_ctx_set_receivers(self.ctx, receivers.data_ptr() if receivers is not None else None))
 
-    def frame_seal(self, desc, receivers, out, stream: int | None = None):
+    def frame_seal(self, desc, receivers, out, in_size: int, max_len: int, stream: int | None = None):
         """wg_frame_seal: write the 16-B transport header {4, 0, 0, 0, receiver_index, counter}
-        in front of every sealed packet (UnencryptedOutgoingTransport.java:14-18,
+        in front of every packet the seal accepts (UnencryptedOutgoingTransport.java:14-18,
         EncryptedOutgoingTransport.java:11-14). `receivers` is a uint32/int32 device tensor
-        indexed by key slot."""
+        indexed by key slot; in_size / max_len are the seal call's."""
         n = desc.shape[0]
         L.check(self._lib.wg_frame_seal(self.ctx, desc.data_ptr(), n, receivers.data_ptr(), out.data_ptr(),
-                                        out.numel(), stream if stream is not None else _torch_stream()))
+                                        out.numel(), in_size, max_len,
+                                        stream if stream is not None else _torch_stream()))
 
     def parse_open(self, wire, pkt_off, pkt_len, key_slot, desc_out, parse_status=None, stream: int | None = None):
         """wg_parse_open: open descriptors from received wire packets on device
@@ -216,6 +240,17 @@ class Engine:
         out = np.zeros(max(n, 1), np.uint8)
         rc = L.check(self._lib.wg_open1(self.ctx, slot, counter, src.ctypes.data, n, out.ctypes.data))
         return None if rc == 1 else out[:n].tobytes()
+
+    def batcher_config(self, max_batch: int = 8192, window_us: int = 0) -> None:
+        """wg_batcher_config: packets per batched launch of seal1/open1 and an optional
+        accumulation window in microseconds."""
+        L.check(self._lib.wg_batcher_config(self.ctx, max_batch, window_us))
+
+    def batcher_stats(self) -> tuple[int, int]:
+        """(launches, packets) issued by the per-packet batcher so far."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        L.check(self._lib.wg_batcher_stats(self.ctx, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
 
     # ---- instrumentation ----------------------------------------------------------
     def timing(self, on: bool):

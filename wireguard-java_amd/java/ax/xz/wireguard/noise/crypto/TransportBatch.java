@@ -2,6 +2,7 @@ package ax.xz.wireguard.noise.crypto;
 
 import java.lang.foreign.Arena;
 import java.lang.foreign.MemorySegment;
+import java.util.concurrent.ForkJoinPool;
 
 import static java.lang.foreign.ValueLayout.*;
 
@@ -26,18 +27,66 @@ public final class TransportBatch {
 		WgAead.releaseKeys(sendSlot, receiveSlot);
 	}
 
+	/**
+	 * One blocking per-packet call. wg_seal1 / wg_open1 wait for the batched launch that
+	 * carries the packet; on a ForkJoinPool worker (TransportManager.java:41 runs every
+	 * packet there) the wait is a ManagedBlocker, so the pool adds workers while callers
+	 * wait and more packets share each launch, without any change in ax.xz.wireguard.
+	 */
+	private static final class Call implements ForkJoinPool.ManagedBlocker {
+		private final boolean open;
+		private final int slot;
+		private final long counter;
+		private final MemorySegment in, out;
+		private final int len;
+		int rc;
+		private boolean done;
+
+		Call(boolean open, int slot, long counter, MemorySegment in, int len, MemorySegment out) {
+			this.open = open;
+			this.slot = slot;
+			this.counter = counter;
+			this.in = in;
+			this.len = len;
+			this.out = out;
+		}
+
+		@Override
+		public boolean block() {
+			try {
+				rc = open ? (int) WgAead.OPEN1.invokeExact(WgAead.CTX, slot, counter, in, len, out)
+				          : (int) WgAead.SEAL1.invokeExact(WgAead.CTX, slot, counter, in, len, out);
+			} catch (Throwable e) {
+				throw new RuntimeException(e);
+			}
+			done = true;
+			return true;
+		}
+
+		@Override
+		public boolean isReleasable() {
+			return done;
+		}
+
+		int run() {
+			try {
+				ForkJoinPool.managedBlock(this);  // off a pool worker this just calls block()
+			} catch (InterruptedException e) {
+				Thread.currentThread().interrupt();
+				throw new RuntimeException(e);
+			}
+			return WgAead.check(rc);
+		}
+	}
+
 	/** dst (len + 16 bytes) = ChaCha20-Poly1305(key[slot], LE64(counter) || 0^4, src). */
 	public static void seal1(int slot, long counter, MemorySegment src, MemorySegment dst) {
 		try (var arena = Arena.ofConfined()) {
 			var in = native_(arena, src);
 			var out = dst.isNative() ? dst : arena.allocate(dst.byteSize(), 16);
-			WgAead.check((int) WgAead.SEAL1.invokeExact(WgAead.CTX, slot, counter, in, (int) src.byteSize(), out));
+			new Call(false, slot, counter, in, (int) src.byteSize(), out).run();
 			if (out != dst)
 				dst.copyFrom(out);
-		} catch (RuntimeException e) {
-			throw e;
-		} catch (Throwable e) {
-			throw new RuntimeException(e);
 		}
 	}
 
@@ -46,16 +95,11 @@ public final class TransportBatch {
 		try (var arena = Arena.ofConfined()) {
 			var in = native_(arena, src);
 			var out = arena.allocate(Math.max(1, dst.byteSize()), 16);
-			int rc = WgAead.check((int) WgAead.OPEN1.invokeExact(WgAead.CTX, slot, counter, in,
-				(int) (src.byteSize() - 16), out));
+			int rc = new Call(true, slot, counter, in, (int) (src.byteSize() - 16), out).run();
 			if (rc != 0)
 				return false;
 			dst.copyFrom(out.asSlice(0, dst.byteSize()));
 			return true;
-		} catch (RuntimeException e) {
-			throw e;
-		} catch (Throwable e) {
-			throw new RuntimeException(e);
 		}
 	}
 

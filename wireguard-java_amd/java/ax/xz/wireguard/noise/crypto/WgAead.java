@@ -59,7 +59,7 @@ public final class WgAead {
 		SYNC = down(linker, symbols, "wg_sync", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS));
 		// device-side wire framing (TransportPacket.java:18-35): header write on seal, header parse on open
 		FRAME_SEAL = down(linker, symbols, "wg_frame_seal", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT,
-			ADDRESS, ADDRESS, JAVA_LONG, ADDRESS));
+			ADDRESS, ADDRESS, JAVA_LONG, JAVA_LONG, JAVA_INT, ADDRESS));
 		PARSE_OPEN = down(linker, symbols, "wg_parse_open", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_LONG,
 			ADDRESS, ADDRESS, ADDRESS, JAVA_INT, ADDRESS, ADDRESS, ADDRESS));
 		SEAL_HOST = down(linker, symbols, "wg_seal_host", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT,
@@ -92,7 +92,7 @@ public final class WgAead {
 		return symbols.find(name).map(addr -> linker.downcallHandle(addr, fd)).orElseThrow();
 	}
 
-	/** Negative return codes become RuntimeExceptions, as the reference's wrappers do (ChaCha20.java:293-295). */
+	/** Negative return codes become RuntimeExceptions, as the reference's wrappers do (ChaCha20.java:102,110,141). */
 	static int check(int rc) {
 		if (rc < 0) {
 			String msg;
@@ -131,8 +131,13 @@ public final class WgAead {
 		return (a << 16) | b;
 	}
 
-	/** SymmetricKeypair.clean: zero both device key slots and release them (SymmetricKeypair.java:85-93). */
+	/**
+	 * SymmetricKeypair.clean: zero both device key slots and release them (SymmetricKeypair.java:85-93).
+	 * Called once per keypair (its Cleanable); a slot that is already free is not released again.
+	 */
 	static void releaseKeys(int send, int receive) {
+		if (FREE_SLOTS.contains(send) || FREE_SLOTS.contains(receive))
+			throw new IllegalStateException("key slots " + send + "/" + receive + " released twice");
 		try {
 			check((int) KEYS_ZERO.invokeExact(CTX, send, 1));
 			check((int) KEYS_ZERO.invokeExact(CTX, receive, 1));

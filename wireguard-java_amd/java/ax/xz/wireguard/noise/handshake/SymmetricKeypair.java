@@ -19,9 +19,15 @@ import java.lang.ref.Cleaner;
  *   <li>decipher(counter, src = ct || tag, dst): AEADBadTagException on a bad tag, dst untouched (:76-83);</li>
  *   <li>clean(): zeroes both keys (:85-93) — here the device key-table slots.</li>
  * </ul>
- * The keys live in the MI355X key table (wg_keys_set); the per-packet calls are
- * synchronous device round trips. {@link #sendBatch()} / {@link #receiveBatch()}
- * expose the additive batch API a batching TransportManager uses (INTEGRATION.md).
+ * The keys live in the MI355X key table (wg_keys_set). The per-packet calls are
+ * synchronous for the caller but batched underneath (wg_seal1 / wg_open1 share
+ * device launches with every concurrent caller; INTEGRATION.md §3).
+ * {@link #claimCounters(int)}, {@link #sendSlot()} and {@link #receiveSlot()} expose
+ * what a batching TransportManager needs for the additive batch API.
+ *
+ * <p>The key slots are released exactly once: {@link #clean()} runs the Cleaner
+ * action itself (Cleanable.clean runs it at most once), so a later garbage collection
+ * cannot release slots that a newer keypair already holds.
  */
 public final class SymmetricKeypair {
 	private static final VarHandle SEND_COUNTER;
@@ -37,6 +43,7 @@ public final class SymmetricKeypair {
 	private static final Cleaner cleaner = Cleaner.create();
 
 	private final int sendSlot, receiveSlot;
+	private final Cleaner.Cleanable cleanable;
 	private volatile long sendCounter = 0;
 	private volatile boolean cleaned = false;
 
@@ -45,16 +52,24 @@ public final class SymmetricKeypair {
 		this.sendSlot = slots >>> 16;
 		this.receiveSlot = slots & 0xffff;
 		int s = sendSlot, r = receiveSlot;
-		cleaner.register(this, () -> TransportBatch.releaseKeys(s, r));
+		// the action must not capture `this`; Cleanable.clean() runs it at most once
+		this.cleanable = cleaner.register(this, () -> TransportBatch.releaseKeys(s, r));
+	}
+
+	private void checkLive() {
+		if (cleaned)  // the reference's keys live in a closed Arena after clean() (:85-93)
+			throw new IllegalStateException("SymmetricKeypair used after clean()");
 	}
 
 	public long cipher(MemorySegment src, MemorySegment dst) {
+		checkLive();
 		var counter = (long) SEND_COUNTER.getAndAdd(this, 1);
 		TransportBatch.seal1(sendSlot, counter, src, dst.asSlice(0, src.byteSize() + 16));
 		return counter;
 	}
 
 	public void decipher(long counter, MemorySegment src, MemorySegment dst) throws BadPaddingException {
+		checkLive();
 		long textLength = src.byteSize() - 16;
 		src.asSlice(textLength, 16);  // IndexOutOfBoundsException for a short src, like the reference
 		if (!TransportBatch.open1(receiveSlot, counter, src, dst.asSlice(0, textLength)))
@@ -75,9 +90,7 @@ public final class SymmetricKeypair {
 	}
 
 	public void clean() {
-		if (!cleaned) {
-			cleaned = true;
-			TransportBatch.releaseKeys(sendSlot, receiveSlot);
-		}
+		cleaned = true;
+		cleanable.clean();  // zeroes and releases both slots, once
 	}
 }

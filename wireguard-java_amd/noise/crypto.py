@@ -66,7 +66,7 @@ class ChaCha20:
 
     @staticmethod
     def initializeState(key, nonce, state, counter: int) -> None:
-        """ChaCha20.java:247-266 (state = constants || key || counter || nonce, LE words)."""
+        """ChaCha20.java:55-74 (state = constants || key || counter || nonce, LE words)."""
         if _size(state) != 64:
             raise ValueError(f"State size must be 64 bytes (is {_size(state)})")
         words = [0x61707865, 0x3320646E, 0x79622D32, 0x6B206574] + list(struct.unpack("<8I", _bytes(key)))
@@ -84,7 +84,7 @@ class ChaCha20:
 
     @staticmethod
     def chacha20Block(state, output, counter: int) -> None:
-        """ChaCha20.java:277-296: sets word 12 = counter and writes one 64-byte keystream block."""
+        """ChaCha20.java:85-104: sets word 12 = counter and writes one 64-byte keystream block."""
         st = bytearray(_bytes(state))
         st[48:52] = struct.pack("<I", counter & 0xFFFFFFFF)
         _write(state, bytes(st))
@@ -93,7 +93,7 @@ class ChaCha20:
 
     @staticmethod
     def chacha20(key, nonce, input, output, counter: int) -> None:
-        """ChaCha20.java:308-335: output = input ^ keystream(counter, counter+1, ...)."""
+        """ChaCha20.java:116-131: output = input ^ keystream(counter, counter+1, ...)."""
         data = _bytes(input)
         if _size(output) < len(data):
             raise ValueError("Output buffer must be at least as large as input buffer")

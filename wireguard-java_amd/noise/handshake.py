@@ -14,7 +14,7 @@ import numpy as np
 
 from .. import _lib as L
 from ..engine import Engine, default_engine, desc_as_int64, pack_desc
-from .crypto import AEADBadTagException, _bytes, _size, _write
+from .crypto import AEADBadTagException, IllegalStateException, _bytes, _size, _write
 
 
 class SymmetricKeypair:
@@ -22,7 +22,9 @@ class SymmetricKeypair:
         """SymmetricKeypair(byte[] sendKeyBytes, byte[] receiveKeyBytes) (SymmetricKeypair.java:39-50)."""
         self._engine = engine or default_engine()
         self._send_slot, self._recv_slot = self._engine.alloc_slots(2)
-        self._engine.set_keys(self._send_slot, bytes(sendKey) + bytes(receiveKey))
+        # one upload per slot: after frees the two claimed slots need not be adjacent
+        self._engine.set_keys(self._send_slot, bytes(sendKey))
+        self._engine.set_keys(self._recv_slot, bytes(receiveKey))
         self._counter = 0  # volatile long sendCounter = 0 (:37)
         self._lock = threading.Lock()
         self._clean = False
@@ -41,8 +43,13 @@ class SymmetricKeypair:
             self._counter += n
             return c
 
+    def _live(self):
+        if self._clean:  # the reference's keys live in a closed Arena after clean() (:85-93)
+            raise IllegalStateException("SymmetricKeypair used after clean()")
+
     def cipher(self, src, dst) -> int:
         """dst = ct || tag (L + 16 bytes); returns the counter used (SymmetricKeypair.java:63-74)."""
+        self._live()
         counter = self._next()
         pt = _bytes(src)
         if _size(dst) < len(pt) + 16:
@@ -52,6 +59,7 @@ class SymmetricKeypair:
 
     def decipher(self, counter: int, src, dst) -> None:
         """src = ct || tag; plaintext of L = |src| - 16 bytes into dst (SymmetricKeypair.java:76-83)."""
+        self._live()
         data = _bytes(src)
         if len(data) < 16:
             raise IndexError("ciphertext shorter than the 16-byte tag")  # asSlice(textLength, 16) fails
@@ -61,16 +69,20 @@ class SymmetricKeypair:
         _write(dst, pt)
 
     def clean(self) -> None:
-        """Zero both keys (SymmetricKeypair.java:85-93)."""
-        if not self._clean:
-            self._engine.free_slots([self._send_slot, self._recv_slot])
+        """Zero both keys (SymmetricKeypair.java:85-93). Runs once: a second clean() is a
+        no-op, so the slots cannot be released twice."""
+        with self._lock:
+            if self._clean:
+                return
             self._clean = True
+        self._engine.free_slots([self._send_slot, self._recv_slot])
 
     # ---- additive batch API (device-resident) --------------------------------------
     def cipher_batch(self, inp, in_offsets, lengths, out, out_offsets, uniform: bool = False, stream=None):
         """Seal n packets of the torch uint8 device buffer `inp` into `out` (ct || tag each).
         Consumes n consecutive counters; returns (first_counter, desc_tensor)."""
         import torch
+        self._live()
         n = len(lengths)
         c0 = self._next(n)
         d = pack_desc(in_offsets, out_offsets, np.arange(c0, c0 + n, dtype=np.uint64), lengths, self._send_slot)
@@ -83,6 +95,7 @@ class SymmetricKeypair:
                        stream=None):
         """Open n packets (ct || tag at in_offsets, L = lengths); returns the device status tensor."""
         import torch
+        self._live()
         n = len(lengths)
         d = pack_desc(in_offsets, out_offsets, counters, lengths, self._recv_slot)
         dt = torch.from_numpy(desc_as_int64(d)).to(inp.device)
