@@ -17,9 +17,12 @@ Workloads (--workload):
                 never the headline value. --host-mem pinned (zero-copy or, with
                 WG_HOST_PATH=copy, the copy pipeline) or pageable (copy pipeline)
 
-Multi-GPU: one process per GPU (torchrun); packets are independent, so each rank
-works on its own shard — no collective on the data path. The only collectives
-are the timing barrier and the max-over-ranks reduction.
+Multi-GPU: one process per GPU; packets are independent, so each rank works on its own
+shard — no collective on the data path. The only collectives are the timing barrier and
+the max-over-ranks reduction. Under torchrun (WORLD_SIZE set) this process is one rank;
+`python bench.py --gpus N` without torchrun starts the N rank processes itself (fresh
+child processes, before anything touches the GPU), waits for them and exits with the
+first failing rank's status. Rank 0 prints the JSON line.
 
 The JSON line also carries:
   roofline      the transport kernel (k_wave, seal and open launches) against the
@@ -209,6 +212,53 @@ def host_bench(args):
     del torch
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """Start one child process per GPU (rank i on GPU i) with the torchrun environment and
+    wait for all of them. Nothing here touches the GPU; the children are new processes."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
+def launch_check(args):
+    """--launch-check: the multi-rank plumbing without a GPU (gloo on CPU): rendezvous,
+    barrier-bracketed timing, max-over-ranks and payload sum, rank 0's JSON line."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (rank + 1))
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        D = importlib.import_module("wireguard-java_amd.dist")
+        (elapsed,), payload, ok = D.reduce_report(dist, "cpu", [elapsed], 1000.0 * (rank + 1), True)
+        dist.barrier()
+        dist.destroy_process_group()
+    else:
+        payload, ok = 1000.0, True
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "elapsed_max": elapsed,
+                          "payload_sum": payload, "ok": ok}), flush=True)
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -223,7 +273,14 @@ def main():
     ap.add_argument("--host-mem", default="pinned", choices=["pinned", "pageable"])
     ap.add_argument("--streams", type=int, default=1)
     ap.add_argument("--kernel", default="default", help="transport kernel (wg_ctx_set_kernel): default|wave1|tile")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}")
+    if args.launch_check:
+        return launch_check(args)
     if args.workload == "c4":
         return host_bench(args)
 

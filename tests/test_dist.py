@@ -107,3 +107,31 @@ def test_gloo_world2_matches_single_process():
     assert merged == single                      # union of shards == unsharded run, byte for byte
     assert (t_max, s_ms, o_ms) == (2.0, 0.5, 2.0)  # max over ranks
     assert payload == TOTAL and ok               # payload summed over ranks
+
+
+def test_bench_spawns_ranks_without_torchrun():
+    """`python bench.py --gpus 2` (no torchrun) starts two rank processes itself; the gloo
+    launch check runs the same rendezvous, barrier, max-over-ranks timing and payload sum
+    as the GPU path and rank 0 alone prints the JSON line."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["ok"]
+    assert out["payload_sum"] == 3000.0          # 1000 (rank 0) + 2000 (rank 1)
+    assert out["elapsed_max"] >= 0.019           # rank 1 sleeps 20 ms: the max, not rank 0's
+
+
+def test_bench_rejects_world_size_mismatch():
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--launch-check"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr

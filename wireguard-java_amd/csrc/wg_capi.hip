@@ -29,6 +29,9 @@
 namespace {
 
 thread_local std::string g_err;
+#ifdef WG_DIAG
+uint64_t* g_stamps = nullptr;
+#endif
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -311,6 +314,9 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
   P.out_size = out_size;
   P.keys = c->keys;
   P.status = status;
+#ifdef WG_DIAG
+  P.stamps = g_stamps;
+#endif
   const uint64_t cap_slots = 8ull * std::max<uint32_t>(c->resident_waves[MODE == WG_MODE_OPEN], wgt::TW);
   uint64_t per_slot = (n + cap_slots - 1) / cap_slots;
   // mixed lengths: a slot holding one packet runs as long as the longest packet, so once a
@@ -320,6 +326,13 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
   const uint32_t waves = (uint32_t)((n + 8ull * per_slot - 1) / (8ull * per_slot));
   const uint32_t grid = (waves + wgt::TW - 1) / wgt::TW;
   P.slots = grid * wgt::TW * 8u;
+  // rounds a slot runs, spread over the 4 issue-priority levels (k_transport)
+  const uint32_t max_rounds = (host_pkt_blocks<WG_MODE_SEAL>(max_len) + 7u) / 8u;
+#ifndef WG_PRIO
+  P.prio_step = 0;
+#else
+  P.prio_step = std::max<uint32_t>(1u, (uint32_t)((per_slot * max_rounds + 3u) / 4u));
+#endif
   bool ordered = false;
   if (!(flags & WG_F_UNIFORM) && per_slot > 1) {  // longest-first order (LPT) for the snake
     int rc;
@@ -354,6 +367,14 @@ hipStream_t pick_stream(wg_ctx*, void* stream) { return (hipStream_t)stream; }
 #include "wg_batcher.hip"
 
 extern "C" {
+
+#ifdef WG_DIAG
+// diagnostic build only: device buffer of 8 x u64 per wave for k_transport phase cycles
+int wg_diag_stamps(void* dev_buf) {
+  g_stamps = (uint64_t*)dev_buf;
+  return WG_OK;
+}
+#endif
 
 const char* wg_last_error(void) { return g_err.c_str(); }
 const char* wg_version(void) { return "wgaead 0.2.0 gfx950"; }

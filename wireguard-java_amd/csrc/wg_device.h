@@ -121,6 +121,7 @@ __device__ __forceinline__ void poly_r_limbs(uint32_t k0, uint32_t k1, uint32_t 
 // carries fit 32 bits) and the wrap carry from d4 is < 2^29.3 (so 5c < 2^32).
 // Each limb's carry seeds the next limb's v_mad_u64_u32 accumulator chain, so a
 // step costs 25 mads + 5 alignbits + 5 ands (+ the 2^130 wrap) and no 64-bit adds.
+#ifndef WG_POLY_ASM
 __device__ __forceinline__ void poly_mul(uint32_t h[5], const uint32_t r[5], const uint32_t s[5]) {
   const uint32_t h0 = h[0], h1 = h[1], h2 = h[2], h3 = h[3], h4 = h[4];
   uint64_t d = (uint64_t)h0 * r[0] + (uint64_t)h1 * s[4] + (uint64_t)h2 * s[3] + (uint64_t)h3 * s[2] +
@@ -143,6 +144,33 @@ __device__ __forceinline__ void poly_mul(uint32_t h[5], const uint32_t r[5], con
   c = h[0] >> 26; h[0] &= M26;
   h[1] += c;
 }
+#else
+// The same product with each v_mad_u64_u32 as an asm statement, so every limb's chain starts
+// from the previous limb's carry (a 64-bit shift pair) instead of the compiler adding the
+// carry to a separately formed chain (2 extra ops per limb).
+__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
+  uint64_t d, cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(cc) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ void poly_mul(uint32_t h[5], const uint32_t r[5], const uint32_t s[5]) {
+  const uint32_t h0 = h[0], h1 = h[1], h2 = h[2], h3 = h[3], h4 = h[4];
+  uint64_t d = mad64(h0, r[0], mad64(h1, s[4], mad64(h2, s[3], mad64(h3, s[2], (uint64_t)h4 * s[1]))));
+  h[0] = (uint32_t)d & M26;
+  d = mad64(h4, s[2], mad64(h3, s[3], mad64(h2, s[4], mad64(h1, r[0], mad64(h0, r[1], d >> 26)))));
+  h[1] = (uint32_t)d & M26;
+  d = mad64(h4, s[3], mad64(h3, s[4], mad64(h2, r[0], mad64(h1, r[1], mad64(h0, r[2], d >> 26)))));
+  h[2] = (uint32_t)d & M26;
+  d = mad64(h4, s[4], mad64(h3, r[0], mad64(h2, r[1], mad64(h1, r[2], mad64(h0, r[3], d >> 26)))));
+  h[3] = (uint32_t)d & M26;
+  d = mad64(h4, r[0], mad64(h3, r[1], mad64(h2, r[2], mad64(h1, r[3], mad64(h0, r[4], d >> 26)))));
+  h[4] = (uint32_t)d & M26;
+  uint32_t c = (uint32_t)(d >> 26);
+  h[0] += c * 5u;
+  c = h[0] >> 26; h[0] &= M26;
+  h[1] += c;
+}
+#endif
 
 // Same product with the five limb sums as independent v_mad_u64_u32 chains
 // (ILP 5) and the carries applied afterwards with 64-bit adds: more instructions

@@ -58,7 +58,32 @@ struct TransportParams {
   uint64_t out_size;
   const uint32_t* keys;   // device key table, 8 words per slot
   uint32_t* status;       // open: per-packet WG_PKT_*
+  uint32_t prio_step;     // rounds per issue-priority level (0: no priority changes)
+#ifdef WG_DIAG
+  uint64_t* stamps;       // diagnostic build only: 10 x u64 per wave (cycles per phase, start/end times)
+#endif
 };
+
+// Per-wave phase accounting, compiled only into the diagnostic library (make diag):
+// cycles spent in each phase of the round loop, summed over the wave's rounds.
+#ifdef WG_DIAG
+#define WG_PH_DECL uint64_t ph_[7] = {0, 0, 0, 0, 0, 0, 0}; uint64_t ph_t = __builtin_amdgcn_s_memtime(); \
+  const uint64_t ph_r0 = __builtin_amdgcn_s_memrealtime(); (void)ph_r0;
+#define WG_PH(k) do { const uint64_t n_ = __builtin_amdgcn_s_memtime(); ph_[k] += n_ - ph_t; ph_t = n_; } while (0)
+#define WG_PH_STORE(idx)                                                                       \
+  do {                                                                                         \
+    if (P.stamps && (threadIdx.x & 63u) == 0) {                                                \
+      uint64_t* o_ = P.stamps + (size_t)(idx) * 10;                                            \
+      for (int k_ = 0; k_ < 7; ++k_) o_[k_] = ph_[k_];                                         \
+      o_[8] = ph_r0;                                                                           \
+      o_[9] = __builtin_amdgcn_s_memrealtime();                                                \
+    }                                                                                          \
+  } while (0)
+#else
+#define WG_PH_DECL
+#define WG_PH(k) do {} while (0)
+#define WG_PH_STORE(idx) do {} while (0)
+#endif
 
 // ---- lane exchange inside an 8-lane slot -------------------------------------------
 // ds_swizzle bitmask mode inside each 32-lane half: src = ((lane & and) | or) ^ xor.
@@ -172,6 +197,8 @@ struct SlotRec {  // per slot, in LDS
 };
 static_assert(sizeof(SlotRec) == 128, "slot record is 128 B");
 
+#define WG_CONST __attribute__((address_space(4)))  // constant address space: scalar loads
+
 __device__ __forceinline__ uint32_t opaque_lane() {
   uint32_t x = threadIdx.x & 63u;
   asm volatile("" : "+v"(x));
@@ -181,6 +208,7 @@ __device__ __forceinline__ uint32_t opaque_lane() {
 template <int MODE>
 __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8))) k_transport(TransportParams P) {
   static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
+  if (P.prio_step) __builtin_amdgcn_s_setprio(3);  // first instruction: a fresh wave is never starved
   __shared__ uint4 img_[TW][4 * 64];     // 4 KB per wave: [chunk q][lane] = the round's payload / MAC input
   __shared__ SlotRec rec_[TW][8];        // 1 KB per wave
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -204,11 +232,31 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
 #pragma unroll
   for (int i = 0; i < 5; ++i) acc[i] = W[i] = 0;
 
+  // Progress-based issue priority: a SIMD arbitrates VALU issue by priority, then age, so with
+  // equal priorities the oldest of its 8 waves runs ahead and the waves finish one after
+  // another, leaving the SIMD with too few waves to hide latency for the last part of the
+  // launch. A wave drops one priority level every prio_step rounds instead, so the waves
+  // that have done the least work issue first and all of them finish close together.
+  uint32_t iter = 0;  // wave-uniform
+  WG_PH_DECL
   while (true) {
+    if (P.prio_step) {
+      const uint32_t lvl = iter / P.prio_step;
+      if (iter % P.prio_step == 0 && lvl <= 3u && lvl > 0u) {
+        if (lvl == 1) __builtin_amdgcn_s_setprio(2);
+        else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
+      ++iter;
+    }
     // ---- slots without a packet take their next one ------------------------------------
     if (!have && nxt != ~0u) {
       const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
       pkt = nxt;
+#ifdef WG_DIAG
+      { uint32_t dn = dnext; asm volatile("s_waitcnt vmcnt(0)" : "+v"(dn)); dnext = dn; }
+      WG_PH(6);
+#endif
       const uint32_t d0 = bcast8<0>(dnext), d1 = bcast8<1>(dnext), d2 = bcast8<2>(dnext), d3 = bcast8<3>(dnext);
       const uint32_t len = bcast8<6>(dnext), ks = bcast8<7>(dnext);
       const uint64_t in_off = (uint64_t)d0 | ((uint64_t)d1 << 32);
@@ -217,7 +265,26 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
           transport_valid<MODE>(in_off, out_off, len, ks, P.max_len, P.key_slots, P.in_size, P.out_size);
       const uintptr_t ia = (uintptr_t)(P.in + in_off), oa = (uintptr_t)(P.out + out_off);
       const uint32_t al = ((ia & 15u) == 0 ? 2u : 0u) | ((oa & 15u) == 0 ? 4u : 0u) | ((oa & 3u) == 0 ? 8u : 0u);
-      if (valid) ((uint32_t*)rec[s].key)[j] = P.keys[8u * ks + j];
+      // The session key. Vector loads come back in order through the CU's L1, so at a launch's
+      // start a key load would queue behind the payload DMA of every wave already running on
+      // the CU; when every slot of the wave uses one key (one session per wave: C1, C3) it comes
+      // through the scalar cache instead, which no payload traffic passes.
+      const uint32_t ks0 = __builtin_amdgcn_readfirstlane(ks);
+      if (!__any(valid && ks != ks0) && ks0 < P.key_slots) {
+        const WG_CONST uint32_t* kp = (const WG_CONST uint32_t*)P.keys + 8u * ks0;
+        uint32_t k[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          k[i] = kp[i];  // s_load_dwordx8
+          asm volatile("" : "+s"(k[i]));  // keep it scalar (no per-lane reload)
+        }
+        uint32_t v = k[0];
+#pragma unroll
+        for (uint32_t i = 1; i < 8u; ++i) v = j == i ? k[i] : v;
+        if (valid) ((uint32_t*)rec[s].key)[j] = v;
+      } else if (valid) {
+        ((uint32_t*)rec[s].key)[j] = P.keys[8u * ks + j];
+      }
       const uint32_t c0 = bcast8<4>(dnext), c1 = bcast8<5>(dnext);  // all 8 lanes active: swizzles read live lanes
       if (j == 0) {
         rec[s].addr = make_uint4(d0, d1, d2, d3);
@@ -233,17 +300,23 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
     }
     if (!__any(have)) break;
     wave_lds_sync();  // the slot records before the lanes read them
+    WG_PH(0);
 
+    // this round's packet parameters, read once (meta = {ctr lo, ctr hi, len, flags})
+    const uint4 meta = rec[opaque_lane() >> 3].meta;
+    const uint32_t len = meta.z;
+    const uint32_t nb = (meta.w & 1u) ? ((len + 63u) >> 6) + 1u : 0u;
     uint32_t x[16];
     {
       // ---- payload prefetch: LDS-DMA straight into this lane's slice of the image ---------
-      // (no registers held across the ARX rounds; unaligned packets load after them)
+      // (no registers held across the ARX rounds)
       const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
-      const uint4 meta = rec[s].meta;
-      const uint32_t len = meta.z;
-      const uint32_t nb = (meta.w & 1u) ? ((len + 63u) >> 6) + 1u : 0u;
       const uint32_t b = 8u * round + j;
+#ifdef WG_ABL_NODMA
+      if (false) {
+#else
       if (have && b < nb && b > 0u) {
+#endif
         const uint32_t off = 64u * (b - 1u);
         const uint32_t nbytes = min(64u, len - off);
         const uint4 ad = rec[s].addr;
@@ -262,7 +335,12 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
         }
       }
       // ---- ChaCha20: block b = 8 round + j ----------------------------------------------
+#ifdef WG_ABL_NOCHACHA  // ablation builds only (timing study; results are wrong)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) x[i] = b * 0x9e3779b9u + (uint32_t)i + meta.x;
+#else
       chacha20_block_lds(rec[s].key, b, meta.x, meta.y, 0u, x);  // every lane (SIMT); act lanes use it
+#endif
     }
 
     if (__any(have && round == 0)) {  // round 0: lane 0 of the slot holds the one-time key r || s
@@ -273,12 +351,10 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
       }
     }
 
+    WG_PH(1);
     // ---- XOR, store, MAC input into the image, one 16-B chunk at a time ----------------------
     {
       const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
-      const uint4 meta = rec[s].meta;
-      const uint32_t len = meta.z;
-      const uint32_t nb = (meta.w & 1u) ? ((len + 63u) >> 6) + 1u : 0u;
       const uint32_t b = 8u * round + j;
       if (have && b < nb && b > 0u) {
         const uint32_t off = 64u * (b - 1u);
@@ -303,12 +379,15 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
               if (cb < 16u) o = mask_chunk(o, cb);
               img[64u * q + lane] = o;  // the MAC input is the ciphertext
             }
+#ifndef WG_ABL_NOSTORE
             store_chunk(dst + 16u * q, cb, o, oal);
+#endif
           }
         }
       }
     }
     wave_lds_sync();
+    WG_PH(2);
 
     // ---- round 0: r^1..r^8 (lane j gets r^(j+1)), R = r^8, W = r^(8-j) --------------------
     // (after the XOR phase, so the 32 registers of keystream and payload are free again)
@@ -342,15 +421,21 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
       wave_lds_sync();
     }
 
+    WG_PH(3);
     // ---- Poly1305 over this round's chunks -------------------------------------------------
-    if (have) {
+#ifdef WG_ABL_NOPOLY
+    if (false) {
+#else
+    if (have && (meta.w & 1u)) {
+#endif
       const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
-      const uint4 meta = rec[s].meta;
-      if (meta.w & 1u) {
-        const uint32_t len = meta.z, nc = (len + 15u) >> 4;
+      {
+        const uint32_t nc = (len + 15u) >> 4;
         const uint32_t M = nc + 1u, D = 8u * ((M + 7u) >> 3) - M;
         const uint32_t c_lo = round ? 32u * round - 4u : 0u;
-        const uint32_t c_end = min(nc, 32u * round + 28u);
+        // chunk nc (after the data) is the length block le64(0) || le64(len): taken here when it
+        // falls inside this round's window, at the finish otherwise
+        const uint32_t c_end = min(nc + 1u, 32u * round + 28u);
         const uint32_t c0 = c_lo + ((j - ((c_lo + D) & 7u)) & 7u);
         // chunk ci of the round sits in lane (ci >> 2) + 1 - 8 round of the slot, row ci & 3
         const uint4* ip = &img[64u * (c0 & 3u) + (lane & ~7u) + ((c0 + 4u) >> 2) - 8u * round];
@@ -360,7 +445,8 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
 #pragma unroll
         for (uint32_t t = 0; t < 4u; ++t) {
           if (c0 + 8u * t < c_end) {
-            const uint4 v = ip[2u * t];
+            uint4 v = ip[2u * t];
+            if (c0 + 8u * t == nc) v = make_uint4(0u, 0u, len, 0u);
             poly_mul(acc, R, Rs);
             uint32_t cl[5];
             poly_block_limbs(v.x, v.y, v.z, v.w, 1u << 24, cl);
@@ -371,21 +457,15 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
       }
     }
 
+    WG_PH(4);
     // ---- finish the packets whose last round this was ---------------------------------------
-    bool done;
-    {
-      const uint4 meta = rec[opaque_lane() >> 3].meta;
-      const uint32_t nb = (meta.w & 1u) ? ((meta.z + 63u) >> 6) + 1u : 0u;
-      done = have && 8u * (round + 1u) >= nb;  // invalid packets (nb = 0) finish at once
-    }
+    const bool done = have && 8u * (round + 1u) >= nb;  // invalid packets (nb = 0) finish at once
     if (__any(done)) {
       if (done) {  // slot-uniform: every lane of a finishing slot is here
         const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
-        const uint4 meta = rec[s].meta;
-        const uint32_t len = meta.z;
         const bool valid = meta.w & 1u;
         if (valid) {
-          if (j == 7u) {  // the length block le64(0) || le64(len) is lane 7's last position
+          if (j == 7u && ((len + 15u) >> 4) >= 32u * round + 28u) {  // length block not taken in the loop
             const uint4 q0 = rec[s].R0, q1 = rec[s].R1, q2 = rec[s].R2;
             const uint32_t R[5] = {q0.x, q0.y, q0.z, q0.w, q1.x};
             const uint32_t Rs[5] = {0u, q1.y, q1.z, q1.w, q2.x};
@@ -440,7 +520,9 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
     }
     if (have) ++round;
     wave_lds_sync();  // this round's image and records before the next round rewrites them
+    WG_PH(5);
   }
+  WG_PH_STORE(blockIdx.x * TW + wv);
 }
 
 // ---- longest-first order for mixed-length batches (LPT) ----------------------------------
