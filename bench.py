@@ -110,22 +110,28 @@ def cpu_baseline(lengths, slots, counters, keys, budget_s: float = 1.5):
     payload = 2.0 * float(L.sum())
 
     def run(th, budget):
-        reps, t0 = 0, time.perf_counter()
+        reps, ts, to, t0 = 0, 0.0, 0.0, time.perf_counter()
         while True:
+            a = time.perf_counter()
             O.seal_batch(desc, inp, ct, keys, threads=th)
+            b = time.perf_counter()
             st = O.open_batch(desc, ct, pt, keys, threads=th)
+            ts += b - a
+            to += time.perf_counter() - b
             reps += 1
-            dt = time.perf_counter() - t0
-            if dt >= budget:
+            if time.perf_counter() - t0 >= budget:
                 assert not st.any()
-                return reps * payload / dt / GIB, reps
+                half = payload / 2
+                return reps * payload / (ts + to) / GIB, reps * half / ts / GIB, reps * half / to / GIB, reps
 
-    multi, reps = run(threads, budget_s)
-    single, _ = run(1, budget_s / 3)
+    multi, m_seal, m_open, reps = run(threads, budget_s)
+    single, s_seal, s_open, _ = run(1, budget_s / 3)
     return {"value": round(multi, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": f"{n} packets of the same workload, seal+open, {reps} reps, oracle/liboracle.so "
                       f"(-O3, bit-exact restatement of the reference C path)",
-            "single_thread": round(single, 3)}
+            "seal": round(m_seal, 3), "open": round(m_open, 3),
+            "single_thread": round(single, 3), "single_thread_seal": round(s_seal, 3),
+            "single_thread_open": round(s_open, 3)}
 
 
 def pmc_valu_insts():

@@ -1,0 +1,118 @@
+/* Per-packet API under load: T caller threads each issue N wg_seal1 / wg_open1 calls
+ * (alternating; each open takes the packet the thread just sealed, so every tag verifies),
+ * the way the reference's ForkJoinPool workers call SymmetricKeypair.cipher / decipher one
+ * packet at a time (TransportManager.java:41,79,152-158). Reports per-call latency
+ * percentiles, the aggregate payload rate and the batcher's mean launch size.
+ *
+ * Build: gcc -O2 -pthread -Iinclude -o tools/batcher_bench tools/batcher_bench.c \
+ *          -Lwireguard-java_amd -l:libwgaead.so -Wl,-rpath,'$ORIGIN/../wireguard-java_amd'
+ * Run:   tools/batcher_bench [threads=16] [calls=10000] [len=1420|0 for mixed 64..1500]
+ * Output: one JSON line. */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "wgaead.h"
+
+static wg_ctx* g_ctx;
+static int g_calls, g_len;
+static double* g_lat;          /* [threads][calls] microseconds */
+static uint64_t* g_bytes;      /* payload bytes per thread */
+static int* g_fail;
+
+static double now_us(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec * 1e6 + t.tv_nsec * 1e-3;
+}
+
+static uint64_t splitmix(uint64_t* s) {
+  uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+static void* worker(void* arg) {
+  const int t = (int)(intptr_t)arg;
+  uint64_t rs = 1000 + t;
+  uint8_t pt[1500], ct[1516], back[1500];
+  for (int i = 0; i < 1500; ++i) pt[i] = (uint8_t)splitmix(&rs);
+  const uint32_t slot = (uint32_t)t % 64u;
+  uint64_t ctr = (uint64_t)t << 40;
+  uint32_t L = 0;
+  for (int i = 0; i < g_calls; ++i) {
+    double t0 = now_us();
+    int rc;
+    if ((i & 1) == 0) {
+      L = g_len ? (uint32_t)g_len : 64u + (uint32_t)(splitmix(&rs) % 1437u);
+      rc = wg_seal1(g_ctx, slot, ctr, pt, L, ct);
+    } else {
+      rc = wg_open1(g_ctx, slot, ctr, ct, L, back);
+      if (rc == 0 && memcmp(back, pt, L) != 0) rc = -100;
+      ++ctr;
+    }
+    g_lat[(size_t)t * g_calls + i] = now_us() - t0;
+    if (rc != 0) ++g_fail[t];
+    g_bytes[t] += L;
+  }
+  return NULL;
+}
+
+static int cmpd(const void* a, const void* b) {
+  double x = *(const double*)a, y = *(const double*)b;
+  return x < y ? -1 : x > y;
+}
+
+int main(int argc, char** argv) {
+  const int T = argc > 1 ? atoi(argv[1]) : 16;
+  g_calls = argc > 2 ? atoi(argv[2]) : 10000;
+  g_len = argc > 3 ? atoi(argv[3]) : 1420;
+  if (T < 1 || T > 1024 || g_calls < 2 || g_len < 0 || g_len > 1500) {
+    fprintf(stderr, "usage: batcher_bench [threads] [calls] [len 0..1500]\n");
+    return 2;
+  }
+  if (wg_ctx_create(0, 64, &g_ctx) != WG_OK) {
+    fprintf(stderr, "wg_ctx_create: %s\n", wg_last_error());
+    return 1;
+  }
+  uint8_t keys[64 * 32];
+  uint64_t ks = 7;
+  for (int i = 0; i < 64 * 32; ++i) keys[i] = (uint8_t)splitmix(&ks);
+  wg_keys_set(g_ctx, 0, 64, keys);
+  g_lat = calloc((size_t)T * g_calls, sizeof(double));
+  g_bytes = calloc(T, sizeof(uint64_t));
+  g_fail = calloc(T, sizeof(int));
+  pthread_t th[1024];
+  /* warm-up: one call per thread, untimed */
+  { uint8_t a[64], b[80]; memset(a, 1, 64); wg_seal1(g_ctx, 0, 1ull << 60, a, 64, b); }
+  uint64_t l0 = 0, p0 = 0;
+  wg_batcher_stats(g_ctx, &l0, &p0);
+  double t0 = now_us();
+  for (int t = 0; t < T; ++t) pthread_create(&th[t], NULL, worker, (void*)(intptr_t)t);
+  for (int t = 0; t < T; ++t) pthread_join(th[t], NULL);
+  double wall = now_us() - t0;
+  uint64_t l1 = 0, p1 = 0;
+  wg_batcher_stats(g_ctx, &l1, &p1);
+  size_t n = (size_t)T * g_calls;
+  qsort(g_lat, n, sizeof(double), cmpd);
+  uint64_t bytes = 0;
+  int fails = 0;
+  for (int t = 0; t < T; ++t) {
+    bytes += g_bytes[t];
+    fails += g_fail[t];
+  }
+  printf("{\"tool\": \"batcher_bench\", \"threads\": %d, \"calls_per_thread\": %d, \"len\": \"%s\", "
+         "\"calls\": %zu, \"failures\": %d, \"wall_s\": %.4f, \"calls_per_s\": %.0f, "
+         "\"payload_gib_s\": %.4f, \"lat_us\": {\"p50\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"p999\": %.1f, "
+         "\"max\": %.1f}, \"launches\": %llu, \"mean_batch\": %.1f}\n",
+         T, g_calls, g_len ? argv[3] : "mixed 64..1500", n, fails, wall * 1e-6, n / (wall * 1e-6),
+         bytes / (wall * 1e-6) / (double)(1u << 30), g_lat[n / 2], g_lat[n * 9 / 10], g_lat[n * 99 / 100],
+         g_lat[n * 999 / 1000], g_lat[n - 1], (unsigned long long)(l1 - l0),
+         (l1 > l0) ? (double)(p1 - p0) / (double)(l1 - l0) : 0.0);
+  wg_ctx_destroy(g_ctx);
+  return fails ? 1 : 0;
+}

@@ -93,6 +93,455 @@
   QR4(M##00, M##10, M##20, M##30, M##01, M##11, M##21, M##31, M##02, M##12, M##22, M##32, M##03, M##13, M##23, M##33) \
   QR4(M##00, M##11, M##22, M##33, M##01, M##12, M##23, M##30, M##02, M##13, M##20, M##31, M##03, M##10, M##21, M##32)
 
+
+// the same dependency pattern without the rotates (add/xor only) and rotates alone
+#define QR4_NOROT(a0, b0, c0, d0, a1, b1, c1, d1, a2, b2, c2, d2, a3, b3, c3, d3)                        \
+  "v_add_u32 " a0 ", " a0 ", " b0 "\n v_add_u32 " a1 ", " a1 ", " b1 "\n v_add_u32 " a2 ", " a2 ", " b2 "\n v_add_u32 " a3 ", " a3 ", " b3 "\n" \
+  "v_xor_b32 " d0 ", " d0 ", " a0 "\n v_xor_b32 " d1 ", " d1 ", " a1 "\n v_xor_b32 " d2 ", " d2 ", " a2 "\n v_xor_b32 " d3 ", " d3 ", " a3 "\n" \
+  "v_add_u32 " c0 ", " c0 ", " d0 "\n v_add_u32 " c1 ", " c1 ", " d1 "\n v_add_u32 " c2 ", " c2 ", " d2 "\n v_add_u32 " c3 ", " c3 ", " d3 "\n" \
+  "v_xor_b32 " b0 ", " b0 ", " c0 "\n v_xor_b32 " b1 ", " b1 ", " c1 "\n v_xor_b32 " b2 ", " b2 ", " c2 "\n v_xor_b32 " b3 ", " b3 ", " c3 "\n" \
+  "v_add_u32 " a0 ", " a0 ", " b0 "\n v_add_u32 " a1 ", " a1 ", " b1 "\n v_add_u32 " a2 ", " a2 ", " b2 "\n v_add_u32 " a3 ", " a3 ", " b3 "\n" \
+  "v_xor_b32 " d0 ", " d0 ", " a0 "\n v_xor_b32 " d1 ", " d1 ", " a1 "\n v_xor_b32 " d2 ", " d2 ", " a2 "\n v_xor_b32 " d3 ", " d3 ", " a3 "\n" \
+  "v_add_u32 " c0 ", " c0 ", " d0 "\n v_add_u32 " c1 ", " c1 ", " d1 "\n v_add_u32 " c2 ", " c2 ", " d2 "\n v_add_u32 " c3 ", " c3 ", " d3 "\n" \
+  "v_xor_b32 " b0 ", " b0 ", " c0 "\n v_xor_b32 " b1 ", " b1 ", " c1 "\n v_xor_b32 " b2 ", " b2 ", " c2 "\n v_xor_b32 " b3 ", " b3 ", " c3 "\n"
+#define DR_NOROT(M)                                                                                                       \
+  QR4_NOROT(M##00, M##10, M##20, M##30, M##01, M##11, M##21, M##31, M##02, M##12, M##22, M##32, M##03, M##13, M##23, M##33) \
+  QR4_NOROT(M##00, M##11, M##22, M##33, M##01, M##12, M##23, M##30, M##02, M##13, M##20, M##31, M##03, M##10, M##21, M##32)
+#define ROT16                                                                                             \
+  "v_alignbit_b32 v40, v40, v40, 20\n v_alignbit_b32 v41, v41, v41, 20\n v_alignbit_b32 v42, v42, v42, 20\n v_alignbit_b32 v43, v43, v43, 20\n" \
+  "v_alignbit_b32 v44, v44, v44, 20\n v_alignbit_b32 v45, v45, v45, 20\n v_alignbit_b32 v46, v46, v46, 20\n v_alignbit_b32 v47, v47, v47, 20\n" \
+  "v_alignbit_b32 v48, v48, v48, 20\n v_alignbit_b32 v49, v49, v49, 20\n v_alignbit_b32 v50, v50, v50, 20\n v_alignbit_b32 v51, v51, v51, 20\n" \
+  "v_alignbit_b32 v52, v52, v52, 20\n v_alignbit_b32 v53, v53, v53, 20\n v_alignbit_b32 v54, v54, v54, 20\n v_alignbit_b32 v55, v55, v55, 20\n"
+// add and alignbit alternating, independent (no dependency between neighbours)
+#define MIX16                                                                                             \
+  "v_add_u32 v40, v40, v56\n v_alignbit_b32 v41, v41, v41, 20\n v_add_u32 v42, v42, v57\n v_alignbit_b32 v43, v43, v43, 20\n" \
+  "v_add_u32 v44, v44, v58\n v_alignbit_b32 v45, v45, v45, 20\n v_add_u32 v46, v46, v59\n v_alignbit_b32 v47, v47, v47, 20\n" \
+  "v_add_u32 v48, v48, v60\n v_alignbit_b32 v49, v49, v49, 20\n v_add_u32 v50, v50, v61\n v_alignbit_b32 v51, v51, v51, 20\n" \
+  "v_add_u32 v52, v52, v62\n v_alignbit_b32 v53, v53, v53, 20\n v_add_u32 v54, v54, v63\n v_alignbit_b32 v55, v55, v55, 20\n"
+// add, xor, xor (VOP2) then one alignbit: the ChaCha ratio, independent ops
+#define MIX3_1                                                                                            \
+  "v_add_u32 v40, v40, v56\n v_xor_b32 v41, v41, v57\n v_alignbit_b32 v42, v42, v42, 20\n" \
+  "v_add_u32 v43, v43, v58\n v_xor_b32 v44, v44, v59\n v_alignbit_b32 v45, v45, v45, 20\n" \
+  "v_add_u32 v46, v46, v60\n v_xor_b32 v47, v47, v61\n v_alignbit_b32 v48, v48, v48, 20\n" \
+  "v_add_u32 v49, v49, v62\n v_xor_b32 v50, v50, v63\n v_alignbit_b32 v51, v51, v51, 20\n"
+
+
+// ---- VOP2-only quarter-round variants (generated op lists) --------------------------------
+// rotl(x, n) as three VOP2 ops through a temp; rotl16 of (d ^ a) as two SDWA xors
+#define DR_SHIFT \
+  "v_add_u32_e32 v40, v40, v41\n" \
+  "v_add_u32_e32 v44, v44, v45\n" \
+  "v_add_u32_e32 v48, v48, v49\n" \
+  "v_add_u32_e32 v52, v52, v53\n" \
+  "v_xor_b32_e32 v43, v43, v40\n" \
+  "v_xor_b32_e32 v47, v47, v44\n" \
+  "v_xor_b32_e32 v51, v51, v48\n" \
+  "v_xor_b32_e32 v55, v55, v52\n" \
+  "v_lshlrev_b32_e32 v56, 16, v43\n" \
+  "v_lshlrev_b32_e32 v57, 16, v47\n" \
+  "v_lshlrev_b32_e32 v58, 16, v51\n" \
+  "v_lshlrev_b32_e32 v59, 16, v55\n" \
+  "v_lshrrev_b32_e32 v43, 16, v43\n" \
+  "v_lshrrev_b32_e32 v47, 16, v47\n" \
+  "v_lshrrev_b32_e32 v51, 16, v51\n" \
+  "v_lshrrev_b32_e32 v55, 16, v55\n" \
+  "v_or_b32_e32 v43, v43, v56\n" \
+  "v_or_b32_e32 v47, v47, v57\n" \
+  "v_or_b32_e32 v51, v51, v58\n" \
+  "v_or_b32_e32 v55, v55, v59\n" \
+  "v_add_u32_e32 v42, v42, v43\n" \
+  "v_add_u32_e32 v46, v46, v47\n" \
+  "v_add_u32_e32 v50, v50, v51\n" \
+  "v_add_u32_e32 v54, v54, v55\n" \
+  "v_xor_b32_e32 v41, v41, v42\n" \
+  "v_xor_b32_e32 v45, v45, v46\n" \
+  "v_xor_b32_e32 v49, v49, v50\n" \
+  "v_xor_b32_e32 v53, v53, v54\n" \
+  "v_lshlrev_b32_e32 v56, 12, v41\n" \
+  "v_lshlrev_b32_e32 v57, 12, v45\n" \
+  "v_lshlrev_b32_e32 v58, 12, v49\n" \
+  "v_lshlrev_b32_e32 v59, 12, v53\n" \
+  "v_lshrrev_b32_e32 v41, 20, v41\n" \
+  "v_lshrrev_b32_e32 v45, 20, v45\n" \
+  "v_lshrrev_b32_e32 v49, 20, v49\n" \
+  "v_lshrrev_b32_e32 v53, 20, v53\n" \
+  "v_or_b32_e32 v41, v41, v56\n" \
+  "v_or_b32_e32 v45, v45, v57\n" \
+  "v_or_b32_e32 v49, v49, v58\n" \
+  "v_or_b32_e32 v53, v53, v59\n" \
+  "v_add_u32_e32 v40, v40, v41\n" \
+  "v_add_u32_e32 v44, v44, v45\n" \
+  "v_add_u32_e32 v48, v48, v49\n" \
+  "v_add_u32_e32 v52, v52, v53\n" \
+  "v_xor_b32_e32 v43, v43, v40\n" \
+  "v_xor_b32_e32 v47, v47, v44\n" \
+  "v_xor_b32_e32 v51, v51, v48\n" \
+  "v_xor_b32_e32 v55, v55, v52\n" \
+  "v_lshlrev_b32_e32 v56, 8, v43\n" \
+  "v_lshlrev_b32_e32 v57, 8, v47\n" \
+  "v_lshlrev_b32_e32 v58, 8, v51\n" \
+  "v_lshlrev_b32_e32 v59, 8, v55\n" \
+  "v_lshrrev_b32_e32 v43, 24, v43\n" \
+  "v_lshrrev_b32_e32 v47, 24, v47\n" \
+  "v_lshrrev_b32_e32 v51, 24, v51\n" \
+  "v_lshrrev_b32_e32 v55, 24, v55\n" \
+  "v_or_b32_e32 v43, v43, v56\n" \
+  "v_or_b32_e32 v47, v47, v57\n" \
+  "v_or_b32_e32 v51, v51, v58\n" \
+  "v_or_b32_e32 v55, v55, v59\n" \
+  "v_add_u32_e32 v42, v42, v43\n" \
+  "v_add_u32_e32 v46, v46, v47\n" \
+  "v_add_u32_e32 v50, v50, v51\n" \
+  "v_add_u32_e32 v54, v54, v55\n" \
+  "v_xor_b32_e32 v41, v41, v42\n" \
+  "v_xor_b32_e32 v45, v45, v46\n" \
+  "v_xor_b32_e32 v49, v49, v50\n" \
+  "v_xor_b32_e32 v53, v53, v54\n" \
+  "v_lshlrev_b32_e32 v56, 7, v41\n" \
+  "v_lshlrev_b32_e32 v57, 7, v45\n" \
+  "v_lshlrev_b32_e32 v58, 7, v49\n" \
+  "v_lshlrev_b32_e32 v59, 7, v53\n" \
+  "v_lshrrev_b32_e32 v41, 25, v41\n" \
+  "v_lshrrev_b32_e32 v45, 25, v45\n" \
+  "v_lshrrev_b32_e32 v49, 25, v49\n" \
+  "v_lshrrev_b32_e32 v53, 25, v53\n" \
+  "v_or_b32_e32 v41, v41, v56\n" \
+  "v_or_b32_e32 v45, v45, v57\n" \
+  "v_or_b32_e32 v49, v49, v58\n" \
+  "v_or_b32_e32 v53, v53, v59\n" \
+  "v_add_u32_e32 v40, v40, v45\n" \
+  "v_add_u32_e32 v44, v44, v49\n" \
+  "v_add_u32_e32 v48, v48, v53\n" \
+  "v_add_u32_e32 v52, v52, v41\n" \
+  "v_xor_b32_e32 v55, v55, v40\n" \
+  "v_xor_b32_e32 v43, v43, v44\n" \
+  "v_xor_b32_e32 v47, v47, v48\n" \
+  "v_xor_b32_e32 v51, v51, v52\n" \
+  "v_lshlrev_b32_e32 v56, 16, v55\n" \
+  "v_lshlrev_b32_e32 v57, 16, v43\n" \
+  "v_lshlrev_b32_e32 v58, 16, v47\n" \
+  "v_lshlrev_b32_e32 v59, 16, v51\n" \
+  "v_lshrrev_b32_e32 v55, 16, v55\n" \
+  "v_lshrrev_b32_e32 v43, 16, v43\n" \
+  "v_lshrrev_b32_e32 v47, 16, v47\n" \
+  "v_lshrrev_b32_e32 v51, 16, v51\n" \
+  "v_or_b32_e32 v55, v55, v56\n" \
+  "v_or_b32_e32 v43, v43, v57\n" \
+  "v_or_b32_e32 v47, v47, v58\n" \
+  "v_or_b32_e32 v51, v51, v59\n" \
+  "v_add_u32_e32 v50, v50, v55\n" \
+  "v_add_u32_e32 v54, v54, v43\n" \
+  "v_add_u32_e32 v42, v42, v47\n" \
+  "v_add_u32_e32 v46, v46, v51\n" \
+  "v_xor_b32_e32 v45, v45, v50\n" \
+  "v_xor_b32_e32 v49, v49, v54\n" \
+  "v_xor_b32_e32 v53, v53, v42\n" \
+  "v_xor_b32_e32 v41, v41, v46\n" \
+  "v_lshlrev_b32_e32 v56, 12, v45\n" \
+  "v_lshlrev_b32_e32 v57, 12, v49\n" \
+  "v_lshlrev_b32_e32 v58, 12, v53\n" \
+  "v_lshlrev_b32_e32 v59, 12, v41\n" \
+  "v_lshrrev_b32_e32 v45, 20, v45\n" \
+  "v_lshrrev_b32_e32 v49, 20, v49\n" \
+  "v_lshrrev_b32_e32 v53, 20, v53\n" \
+  "v_lshrrev_b32_e32 v41, 20, v41\n" \
+  "v_or_b32_e32 v45, v45, v56\n" \
+  "v_or_b32_e32 v49, v49, v57\n" \
+  "v_or_b32_e32 v53, v53, v58\n" \
+  "v_or_b32_e32 v41, v41, v59\n" \
+  "v_add_u32_e32 v40, v40, v45\n" \
+  "v_add_u32_e32 v44, v44, v49\n" \
+  "v_add_u32_e32 v48, v48, v53\n" \
+  "v_add_u32_e32 v52, v52, v41\n" \
+  "v_xor_b32_e32 v55, v55, v40\n" \
+  "v_xor_b32_e32 v43, v43, v44\n" \
+  "v_xor_b32_e32 v47, v47, v48\n" \
+  "v_xor_b32_e32 v51, v51, v52\n" \
+  "v_lshlrev_b32_e32 v56, 8, v55\n" \
+  "v_lshlrev_b32_e32 v57, 8, v43\n" \
+  "v_lshlrev_b32_e32 v58, 8, v47\n" \
+  "v_lshlrev_b32_e32 v59, 8, v51\n" \
+  "v_lshrrev_b32_e32 v55, 24, v55\n" \
+  "v_lshrrev_b32_e32 v43, 24, v43\n" \
+  "v_lshrrev_b32_e32 v47, 24, v47\n" \
+  "v_lshrrev_b32_e32 v51, 24, v51\n" \
+  "v_or_b32_e32 v55, v55, v56\n" \
+  "v_or_b32_e32 v43, v43, v57\n" \
+  "v_or_b32_e32 v47, v47, v58\n" \
+  "v_or_b32_e32 v51, v51, v59\n" \
+  "v_add_u32_e32 v50, v50, v55\n" \
+  "v_add_u32_e32 v54, v54, v43\n" \
+  "v_add_u32_e32 v42, v42, v47\n" \
+  "v_add_u32_e32 v46, v46, v51\n" \
+  "v_xor_b32_e32 v45, v45, v50\n" \
+  "v_xor_b32_e32 v49, v49, v54\n" \
+  "v_xor_b32_e32 v53, v53, v42\n" \
+  "v_xor_b32_e32 v41, v41, v46\n" \
+  "v_lshlrev_b32_e32 v56, 7, v45\n" \
+  "v_lshlrev_b32_e32 v57, 7, v49\n" \
+  "v_lshlrev_b32_e32 v58, 7, v53\n" \
+  "v_lshlrev_b32_e32 v59, 7, v41\n" \
+  "v_lshrrev_b32_e32 v45, 25, v45\n" \
+  "v_lshrrev_b32_e32 v49, 25, v49\n" \
+  "v_lshrrev_b32_e32 v53, 25, v53\n" \
+  "v_lshrrev_b32_e32 v41, 25, v41\n" \
+  "v_or_b32_e32 v45, v45, v56\n" \
+  "v_or_b32_e32 v49, v49, v57\n" \
+  "v_or_b32_e32 v53, v53, v58\n" \
+  "v_or_b32_e32 v41, v41, v59\n"
+constexpr int DR_SHIFT_n = 160;
+#define DR_SDWA \
+  "v_add_u32_e32 v40, v40, v41\n" \
+  "v_add_u32_e32 v44, v44, v45\n" \
+  "v_add_u32_e32 v48, v48, v49\n" \
+  "v_add_u32_e32 v52, v52, v53\n" \
+  "v_xor_b32_sdwa v56, v43, v40 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0\n" \
+  "v_xor_b32_sdwa v57, v47, v44 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0\n" \
+  "v_xor_b32_sdwa v58, v51, v48 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0\n" \
+  "v_xor_b32_sdwa v59, v55, v52 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0\n" \
+  "v_xor_b32_sdwa v56, v43, v40 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1\n" \
+  "v_xor_b32_sdwa v57, v47, v44 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1\n" \
+  "v_xor_b32_sdwa v58, v51, v48 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1\n" \
+  "v_xor_b32_sdwa v59, v55, v52 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1\n" \
+  "v_mov_b32_e32 v43, v56\n" \
+  "v_mov_b32_e32 v47, v57\n" \
+  "v_mov_b32_e32 v51, v58\n" \
+  "v_mov_b32_e32 v55, v59\n" \
+  "v_add_u32_e32 v42, v42, v43\n" \
+  "v_add_u32_e32 v46, v46, v47\n" \
+  "v_add_u32_e32 v50, v50, v51\n" \
+  "v_add_u32_e32 v54, v54, v55\n" \
+  "v_xor_b32_e32 v41, v41, v42\n" \
+  "v_xor_b32_e32 v45, v45, v46\n" \
+  "v_xor_b32_e32 v49, v49, v50\n" \
+  "v_xor_b32_e32 v53, v53, v54\n" \
+  "v_lshlrev_b32_e32 v56, 12, v41\n" \
+  "v_lshlrev_b32_e32 v57, 12, v45\n" \
+  "v_lshlrev_b32_e32 v58, 12, v49\n" \
+  "v_lshlrev_b32_e32 v59, 12, v53\n" \
+  "v_lshrrev_b32_e32 v41, 20, v41\n" \
+  "v_lshrrev_b32_e32 v45, 20, v45\n" \
+  "v_lshrrev_b32_e32 v49, 20, v49\n" \
+  "v_lshrrev_b32_e32 v53, 20, v53\n" \
+  "v_or_b32_e32 v41, v41, v56\n" \
+  "v_or_b32_e32 v45, v45, v57\n" \
+  "v_or_b32_e32 v49, v49, v58\n" \
+  "v_or_b32_e32 v53, v53, v59\n" \
+  "v_add_u32_e32 v40, v40, v41\n" \
+  "v_add_u32_e32 v44, v44, v45\n" \
+  "v_add_u32_e32 v48, v48, v49\n" \
+  "v_add_u32_e32 v52, v52, v53\n" \
+  "v_xor_b32_e32 v43, v43, v40\n" \
+  "v_xor_b32_e32 v47, v47, v44\n" \
+  "v_xor_b32_e32 v51, v51, v48\n" \
+  "v_xor_b32_e32 v55, v55, v52\n" \
+  "v_lshlrev_b32_e32 v56, 8, v43\n" \
+  "v_lshlrev_b32_e32 v57, 8, v47\n" \
+  "v_lshlrev_b32_e32 v58, 8, v51\n" \
+  "v_lshlrev_b32_e32 v59, 8, v55\n" \
+  "v_lshrrev_b32_e32 v43, 24, v43\n" \
+  "v_lshrrev_b32_e32 v47, 24, v47\n" \
+  "v_lshrrev_b32_e32 v51, 24, v51\n" \
+  "v_lshrrev_b32_e32 v55, 24, v55\n" \
+  "v_or_b32_e32 v43, v43, v56\n" \
+  "v_or_b32_e32 v47, v47, v57\n" \
+  "v_or_b32_e32 v51, v51, v58\n" \
+  "v_or_b32_e32 v55, v55, v59\n" \
+  "v_add_u32_e32 v42, v42, v43\n" \
+  "v_add_u32_e32 v46, v46, v47\n" \
+  "v_add_u32_e32 v50, v50, v51\n" \
+  "v_add_u32_e32 v54, v54, v55\n" \
+  "v_xor_b32_e32 v41, v41, v42\n" \
+  "v_xor_b32_e32 v45, v45, v46\n" \
+  "v_xor_b32_e32 v49, v49, v50\n" \
+  "v_xor_b32_e32 v53, v53, v54\n" \
+  "v_lshlrev_b32_e32 v56, 7, v41\n" \
+  "v_lshlrev_b32_e32 v57, 7, v45\n" \
+  "v_lshlrev_b32_e32 v58, 7, v49\n" \
+  "v_lshlrev_b32_e32 v59, 7, v53\n" \
+  "v_lshrrev_b32_e32 v41, 25, v41\n" \
+  "v_lshrrev_b32_e32 v45, 25, v45\n" \
+  "v_lshrrev_b32_e32 v49, 25, v49\n" \
+  "v_lshrrev_b32_e32 v53, 25, v53\n" \
+  "v_or_b32_e32 v41, v41, v56\n" \
+  "v_or_b32_e32 v45, v45, v57\n" \
+  "v_or_b32_e32 v49, v49, v58\n" \
+  "v_or_b32_e32 v53, v53, v59\n" \
+  "v_add_u32_e32 v40, v40, v45\n" \
+  "v_add_u32_e32 v44, v44, v49\n" \
+  "v_add_u32_e32 v48, v48, v53\n" \
+  "v_add_u32_e32 v52, v52, v41\n" \
+  "v_xor_b32_sdwa v56, v55, v40 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0\n" \
+  "v_xor_b32_sdwa v57, v43, v44 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0\n" \
+  "v_xor_b32_sdwa v58, v47, v48 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0\n" \
+  "v_xor_b32_sdwa v59, v51, v52 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:WORD_0\n" \
+  "v_xor_b32_sdwa v56, v55, v40 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1\n" \
+  "v_xor_b32_sdwa v57, v43, v44 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1\n" \
+  "v_xor_b32_sdwa v58, v47, v48 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1\n" \
+  "v_xor_b32_sdwa v59, v51, v52 dst_sel:WORD_0 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1\n" \
+  "v_mov_b32_e32 v55, v56\n" \
+  "v_mov_b32_e32 v43, v57\n" \
+  "v_mov_b32_e32 v47, v58\n" \
+  "v_mov_b32_e32 v51, v59\n" \
+  "v_add_u32_e32 v50, v50, v55\n" \
+  "v_add_u32_e32 v54, v54, v43\n" \
+  "v_add_u32_e32 v42, v42, v47\n" \
+  "v_add_u32_e32 v46, v46, v51\n" \
+  "v_xor_b32_e32 v45, v45, v50\n" \
+  "v_xor_b32_e32 v49, v49, v54\n" \
+  "v_xor_b32_e32 v53, v53, v42\n" \
+  "v_xor_b32_e32 v41, v41, v46\n" \
+  "v_lshlrev_b32_e32 v56, 12, v45\n" \
+  "v_lshlrev_b32_e32 v57, 12, v49\n" \
+  "v_lshlrev_b32_e32 v58, 12, v53\n" \
+  "v_lshlrev_b32_e32 v59, 12, v41\n" \
+  "v_lshrrev_b32_e32 v45, 20, v45\n" \
+  "v_lshrrev_b32_e32 v49, 20, v49\n" \
+  "v_lshrrev_b32_e32 v53, 20, v53\n" \
+  "v_lshrrev_b32_e32 v41, 20, v41\n" \
+  "v_or_b32_e32 v45, v45, v56\n" \
+  "v_or_b32_e32 v49, v49, v57\n" \
+  "v_or_b32_e32 v53, v53, v58\n" \
+  "v_or_b32_e32 v41, v41, v59\n" \
+  "v_add_u32_e32 v40, v40, v45\n" \
+  "v_add_u32_e32 v44, v44, v49\n" \
+  "v_add_u32_e32 v48, v48, v53\n" \
+  "v_add_u32_e32 v52, v52, v41\n" \
+  "v_xor_b32_e32 v55, v55, v40\n" \
+  "v_xor_b32_e32 v43, v43, v44\n" \
+  "v_xor_b32_e32 v47, v47, v48\n" \
+  "v_xor_b32_e32 v51, v51, v52\n" \
+  "v_lshlrev_b32_e32 v56, 8, v55\n" \
+  "v_lshlrev_b32_e32 v57, 8, v43\n" \
+  "v_lshlrev_b32_e32 v58, 8, v47\n" \
+  "v_lshlrev_b32_e32 v59, 8, v51\n" \
+  "v_lshrrev_b32_e32 v55, 24, v55\n" \
+  "v_lshrrev_b32_e32 v43, 24, v43\n" \
+  "v_lshrrev_b32_e32 v47, 24, v47\n" \
+  "v_lshrrev_b32_e32 v51, 24, v51\n" \
+  "v_or_b32_e32 v55, v55, v56\n" \
+  "v_or_b32_e32 v43, v43, v57\n" \
+  "v_or_b32_e32 v47, v47, v58\n" \
+  "v_or_b32_e32 v51, v51, v59\n" \
+  "v_add_u32_e32 v50, v50, v55\n" \
+  "v_add_u32_e32 v54, v54, v43\n" \
+  "v_add_u32_e32 v42, v42, v47\n" \
+  "v_add_u32_e32 v46, v46, v51\n" \
+  "v_xor_b32_e32 v45, v45, v50\n" \
+  "v_xor_b32_e32 v49, v49, v54\n" \
+  "v_xor_b32_e32 v53, v53, v42\n" \
+  "v_xor_b32_e32 v41, v41, v46\n" \
+  "v_lshlrev_b32_e32 v56, 7, v45\n" \
+  "v_lshlrev_b32_e32 v57, 7, v49\n" \
+  "v_lshlrev_b32_e32 v58, 7, v53\n" \
+  "v_lshlrev_b32_e32 v59, 7, v41\n" \
+  "v_lshrrev_b32_e32 v45, 25, v45\n" \
+  "v_lshrrev_b32_e32 v49, 25, v49\n" \
+  "v_lshrrev_b32_e32 v53, 25, v53\n" \
+  "v_lshrrev_b32_e32 v41, 25, v41\n" \
+  "v_or_b32_e32 v45, v45, v56\n" \
+  "v_or_b32_e32 v49, v49, v57\n" \
+  "v_or_b32_e32 v53, v53, v58\n" \
+  "v_or_b32_e32 v41, v41, v59\n"
+constexpr int DR_SDWA_n = 152;
+#define DR_ALIGN2 \
+  "v_add_u32_e32 v40, v40, v41\n" \
+  "v_add_u32_e32 v44, v44, v45\n" \
+  "v_add_u32_e32 v48, v48, v49\n" \
+  "v_add_u32_e32 v52, v52, v53\n" \
+  "v_xor_b32_e32 v43, v43, v40\n" \
+  "v_xor_b32_e32 v47, v47, v44\n" \
+  "v_xor_b32_e32 v51, v51, v48\n" \
+  "v_xor_b32_e32 v55, v55, v52\n" \
+  "v_alignbit_b32 v43, v43, v43, 16\n" \
+  "v_alignbit_b32 v47, v47, v47, 16\n" \
+  "v_alignbit_b32 v51, v51, v51, 16\n" \
+  "v_alignbit_b32 v55, v55, v55, 16\n" \
+  "v_add_u32_e32 v42, v42, v43\n" \
+  "v_add_u32_e32 v46, v46, v47\n" \
+  "v_add_u32_e32 v50, v50, v51\n" \
+  "v_add_u32_e32 v54, v54, v55\n" \
+  "v_xor_b32_e32 v41, v41, v42\n" \
+  "v_xor_b32_e32 v45, v45, v46\n" \
+  "v_xor_b32_e32 v49, v49, v50\n" \
+  "v_xor_b32_e32 v53, v53, v54\n" \
+  "v_alignbit_b32 v41, v41, v41, 20\n" \
+  "v_alignbit_b32 v45, v45, v45, 20\n" \
+  "v_alignbit_b32 v49, v49, v49, 20\n" \
+  "v_alignbit_b32 v53, v53, v53, 20\n" \
+  "v_add_u32_e32 v40, v40, v41\n" \
+  "v_add_u32_e32 v44, v44, v45\n" \
+  "v_add_u32_e32 v48, v48, v49\n" \
+  "v_add_u32_e32 v52, v52, v53\n" \
+  "v_xor_b32_e32 v43, v43, v40\n" \
+  "v_xor_b32_e32 v47, v47, v44\n" \
+  "v_xor_b32_e32 v51, v51, v48\n" \
+  "v_xor_b32_e32 v55, v55, v52\n" \
+  "v_alignbit_b32 v43, v43, v43, 24\n" \
+  "v_alignbit_b32 v47, v47, v47, 24\n" \
+  "v_alignbit_b32 v51, v51, v51, 24\n" \
+  "v_alignbit_b32 v55, v55, v55, 24\n" \
+  "v_add_u32_e32 v42, v42, v43\n" \
+  "v_add_u32_e32 v46, v46, v47\n" \
+  "v_add_u32_e32 v50, v50, v51\n" \
+  "v_add_u32_e32 v54, v54, v55\n" \
+  "v_xor_b32_e32 v41, v41, v42\n" \
+  "v_xor_b32_e32 v45, v45, v46\n" \
+  "v_xor_b32_e32 v49, v49, v50\n" \
+  "v_xor_b32_e32 v53, v53, v54\n" \
+  "v_alignbit_b32 v41, v41, v41, 25\n" \
+  "v_alignbit_b32 v45, v45, v45, 25\n" \
+  "v_alignbit_b32 v49, v49, v49, 25\n" \
+  "v_alignbit_b32 v53, v53, v53, 25\n" \
+  "v_add_u32_e32 v40, v40, v45\n" \
+  "v_add_u32_e32 v44, v44, v49\n" \
+  "v_add_u32_e32 v48, v48, v53\n" \
+  "v_add_u32_e32 v52, v52, v41\n" \
+  "v_xor_b32_e32 v55, v55, v40\n" \
+  "v_xor_b32_e32 v43, v43, v44\n" \
+  "v_xor_b32_e32 v47, v47, v48\n" \
+  "v_xor_b32_e32 v51, v51, v52\n" \
+  "v_alignbit_b32 v55, v55, v55, 16\n" \
+  "v_alignbit_b32 v43, v43, v43, 16\n" \
+  "v_alignbit_b32 v47, v47, v47, 16\n" \
+  "v_alignbit_b32 v51, v51, v51, 16\n" \
+  "v_add_u32_e32 v50, v50, v55\n" \
+  "v_add_u32_e32 v54, v54, v43\n" \
+  "v_add_u32_e32 v42, v42, v47\n" \
+  "v_add_u32_e32 v46, v46, v51\n" \
+  "v_xor_b32_e32 v45, v45, v50\n" \
+  "v_xor_b32_e32 v49, v49, v54\n" \
+  "v_xor_b32_e32 v53, v53, v42\n" \
+  "v_xor_b32_e32 v41, v41, v46\n" \
+  "v_alignbit_b32 v45, v45, v45, 20\n" \
+  "v_alignbit_b32 v49, v49, v49, 20\n" \
+  "v_alignbit_b32 v53, v53, v53, 20\n" \
+  "v_alignbit_b32 v41, v41, v41, 20\n" \
+  "v_add_u32_e32 v40, v40, v45\n" \
+  "v_add_u32_e32 v44, v44, v49\n" \
+  "v_add_u32_e32 v48, v48, v53\n" \
+  "v_add_u32_e32 v52, v52, v41\n" \
+  "v_xor_b32_e32 v55, v55, v40\n" \
+  "v_xor_b32_e32 v43, v43, v44\n" \
+  "v_xor_b32_e32 v47, v47, v48\n" \
+  "v_xor_b32_e32 v51, v51, v52\n" \
+  "v_alignbit_b32 v55, v55, v55, 24\n" \
+  "v_alignbit_b32 v43, v43, v43, 24\n" \
+  "v_alignbit_b32 v47, v47, v47, 24\n" \
+  "v_alignbit_b32 v51, v51, v51, 24\n" \
+  "v_add_u32_e32 v50, v50, v55\n" \
+  "v_add_u32_e32 v54, v54, v43\n" \
+  "v_add_u32_e32 v42, v42, v47\n" \
+  "v_add_u32_e32 v46, v46, v51\n" \
+  "v_xor_b32_e32 v45, v45, v50\n" \
+  "v_xor_b32_e32 v49, v49, v54\n" \
+  "v_xor_b32_e32 v53, v53, v42\n" \
+  "v_xor_b32_e32 v41, v41, v46\n" \
+  "v_alignbit_b32 v45, v45, v45, 25\n" \
+  "v_alignbit_b32 v49, v49, v49, 25\n" \
+  "v_alignbit_b32 v53, v53, v53, 25\n" \
+  "v_alignbit_b32 v41, v41, v41, 25\n"
+constexpr int DR_ALIGN2_n = 96;
 #define CLOB                                                                                                     \
   "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", \
       "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63"
@@ -115,6 +564,13 @@ KERNEL(k_add_same, ADD_SAME ADD_SAME ADD_SAME ADD_SAME, 64)
 KERNEL(k_add_diff, ADD_DIFF ADD_DIFF ADD_DIFF ADD_DIFF, 64)
 KERNEL(k_qr_row, DR(R) DR(R), 192)
 KERNEL(k_qr_col, DR(C) DR(C), 192)
+KERNEL(k_qr_norot, DR_NOROT(R) DR_NOROT(R), 128)
+KERNEL(k_rot, ROT16 ROT16 ROT16 ROT16, 64)
+KERNEL(k_mix16, MIX16 MIX16 MIX16 MIX16, 64)
+KERNEL(k_mix3, MIX3_1 MIX3_1 MIX3_1 MIX3_1, 48)
+KERNEL(k_dr_shift, DR_SHIFT DR_SHIFT, 2 * DR_SHIFT_n)
+KERNEL(k_dr_sdwa, DR_SDWA DR_SDWA, 2 * DR_SDWA_n)
+KERNEL(k_dr_align, DR_ALIGN2 DR_ALIGN2, 2 * DR_ALIGN2_n)
 
 int main() {
   hipDeviceProp_t p;
@@ -142,12 +598,20 @@ int main() {
     (void)hipMemcpy(&c, clk, 8, hipMemcpyDeviceToHost);
     const double wave_inst_per_simd = (double)iters * n * 8.0;  // 8 waves per SIMD
     const double cyc = (double)c;                                // shader cycles of one wave's loop
-    printf("%-10s %8.3f ms/launch  %6.3f cycles per wave-instruction per SIMD (s_memtime)  %6.3f at 2.4 GHz\n", nm,
+    printf("%-10s %5d inst %8.3f ms/launch  %6.3f cycles per wave-instruction per SIMD (s_memtime)  %6.3f at 2.4 GHz\n", nm, n,
            ms / reps, cyc / wave_inst_per_simd, ms / reps * 1e-3 * 2.4e9 / wave_inst_per_simd);
   };
   run("add_same", k_add_same, k_add_same_n);
   run("add_diff", k_add_diff, k_add_diff_n);
   run("qr_row", k_qr_row, k_qr_row_n);
   run("qr_col", k_qr_col, k_qr_col_n);
+  run("qr_norot", k_qr_norot, k_qr_norot_n);
+  run("rot", k_rot, k_rot_n);
+  run("add|rot", k_mix16, k_mix16_n);
+  run("add,xor,rot", k_mix3, k_mix3_n);
+  // per double round (96 ChaCha ops): time per DR = n * cycles
+  run("dr_shift", k_dr_shift, k_dr_shift_n);
+  run("dr_sdwa", k_dr_sdwa, k_dr_sdwa_n);
+  run("dr_align", k_dr_align, k_dr_align_n);
   return 0;
 }

@@ -41,13 +41,14 @@ struct BatchBuf {
   uint32_t writers = 0;  // reserved entries still being filled by their callers
   uint32_t users = 0;    // entries whose callers have not yet read their result
   std::chrono::steady_clock::time_point first;
+  std::atomic<uint64_t> done_gen{0};  // gen of the last completed launch from this buffer
+  std::condition_variable cv_done;    // this buffer's callers: their batch completed
 };
 
 struct Batcher {
   wg_ctx* c = nullptr;
   std::mutex mu;
   std::condition_variable cv_work;  // launcher: entries arrived / writers done / stop
-  std::condition_variable cv_done;  // callers: their batch completed
   std::condition_variable cv_free;  // callers: room in a fresh open batch
   BatchBuf buf[kBatchBufs];
   int open_idx = 0;
@@ -58,7 +59,8 @@ struct Batcher {
   int launch_error = WG_OK;
   std::string launch_msg;
   uint64_t launches = 0, packets = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // seal launches
+  hipStream_t stream2 = nullptr;  // open launches
   std::thread th;
 };
 
@@ -69,21 +71,36 @@ void batcher_free_mem(Batcher* B) {
     for (void* p : {(void*)b.sdesc, (void*)b.odesc, (void*)b.in, (void*)b.out, (void*)b.status})
       if (p) (void)hipHostFree(p);
   if (B->stream) (void)hipStreamDestroy(B->stream);
+  if (B->stream2) (void)hipStreamDestroy(B->stream2);
 }
 
 int batcher_launch(Batcher* B, BatchBuf& b) {
   wg_ctx* c = B->c;
   std::lock_guard<std::mutex> lk(c->mu);
   int rc = WG_OK;
+  // seal and open entries are independent: two launches on two streams run side by side
+  // (a small batch's launch is latency-bound, so this halves the batch round trip)
   if (b.nseal)
     rc = launch_transport<WG_MODE_SEAL>(c, b.d_sdesc, b.nseal, b.d_in, kBatchArena, b.d_out, kBatchArena, nullptr,
                                        b.seal_max, 0, B->stream);
   if (rc == WG_OK && b.nopen)
     rc = launch_transport<WG_MODE_OPEN>(c, b.d_odesc, b.nopen, b.d_in, kBatchArena, b.d_out, kBatchArena,
-                                       b.d_status, b.open_max, 0, B->stream);
-  if (rc == WG_OK) {
-    const hipError_t e = hipStreamSynchronize(B->stream);
-    if (e != hipSuccess) rc = fail(WG_EDEVICE, "batch sync: %s", hipGetErrorString(e));
+                                       b.d_status, b.open_max, 0, B->stream2);
+  // wait by polling: a blocking synchronize sleeps on an interrupt and adds tens of µs to
+  // every batch round trip; the launcher thread spins while its batch is on the device
+  const bool used[2] = {b.nseal > 0, b.nopen > 0};
+  const hipStream_t st[2] = {B->stream, B->stream2};
+  for (int k = 0; k < 2; ++k) {
+    if (!used[k]) continue;
+    const auto t0 = std::chrono::steady_clock::now();
+    hipError_t e;
+    while ((e = hipStreamQuery(st[k])) == hipErrorNotReady) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+        e = hipStreamSynchronize(st[k]);  // long batch: stop spinning
+        break;
+      }
+    }
+    if (e != hipSuccess && rc == WG_OK) rc = fail(WG_EDEVICE, "batch sync: %s", hipGetErrorString(e));
   }
   return rc;
 }
@@ -128,7 +145,8 @@ void batcher_loop(Batcher* B) {
     B->launches += 1;
     B->packets += b->nseal + b->nopen;
     b->state = b->users ? BatchBuf::DONE : BatchBuf::FREE;
-    B->cv_done.notify_all();
+    b->done_gen.store(b->gen, std::memory_order_release);
+    b->cv_done.notify_all();
     B->cv_free.notify_all();
   }
 }
@@ -142,7 +160,8 @@ int batcher_get(wg_ctx* c, Batcher** out) {
   DeviceGuard g(c->device);
   Batcher* B = new Batcher();
   B->c = c;
-  bool ok = hipStreamCreateWithFlags(&B->stream, hipStreamNonBlocking) == hipSuccess;
+  bool ok = hipStreamCreateWithFlags(&B->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&B->stream2, hipStreamNonBlocking) == hipSuccess;
   const unsigned fl = hipHostMallocMapped | hipHostMallocPortable;
   for (BatchBuf& b : B->buf) {
     if (!ok) break;
@@ -226,8 +245,8 @@ int batcher_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, co
   (open ? b->odesc : b->sdesc)[idx] = d;
   lk.lock();
   b->writers -= 1;
-  B->cv_work.notify_one();
-  B->cv_done.wait(lk, [&] { return b->gen == gen && b->state == BatchBuf::DONE; });
+  if (b->writers == 0 || b->nseal + b->nopen == 1) B->cv_work.notify_one();
+  b->cv_done.wait(lk, [&] { return b->done_gen.load(std::memory_order_acquire) == gen; });
   rc = B->launch_error;
   const std::string msg = B->launch_msg;
   lk.unlock();

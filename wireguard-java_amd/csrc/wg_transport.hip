@@ -79,6 +79,10 @@ struct TransportParams {
       o_[9] = __builtin_amdgcn_s_memrealtime();                                                \
     }                                                                                          \
   } while (0)
+#elif defined(WG_MARKS)  // asm comments at the phase boundaries (tools/isa_phases.py)
+#define WG_PH_DECL
+#define WG_PH(k) asm volatile(";; WGMARK " #k)
+#define WG_PH_STORE(idx) do {} while (0)
 #else
 #define WG_PH_DECL
 #define WG_PH(k) do {} while (0)
