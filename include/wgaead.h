@@ -44,6 +44,12 @@ extern "C" {
 
 #define WG_PKT_OK 0u
 #define WG_PKT_BADTAG 1u
+/* (2 = WG_PKT_BADHDR, the parse status of wg_parse_open) */
+/* written by wg_rx_check (receive-side checks after open; only WG_PKT_OK packets are examined) */
+#define WG_PKT_KEEPALIVE 3u /* zero-length plaintext: a keepalive, not forwarded */
+#define WG_PKT_BADIP 4u     /* IP version nibble not 4 or 6, or too short for the destination address */
+#define WG_PKT_FILTERED 5u  /* destination outside the key slot's AllowedIPs filter */
+#define WG_PKT_REPLAY 6u    /* counter replayed, too old for the window, or >= 2^64 - 2^13 - 1 */
 
 #define WG_TAG_SIZE 16   /* Crypto.ChaChaPoly1305Overhead (NOISE/crypto/Crypto.java:14) */
 #define WG_NONCE_SIZE 12 /* Crypto.ChaChaPoly1305NonceSize (NOISE/crypto/Crypto.java:13) */
@@ -213,6 +219,56 @@ int wg_parse_open(wg_ctx* ctx, const uint8_t* wire_dev, uint64_t wire_size, cons
  *   to `out_host` (bytes between packets — wire headers, ring slack — are kept).
  *   On a bad tag the plaintext range is zero-filled and status[i] = WG_PKT_BADTAG.
  *   flags: WG_F_UNIFORM only. */
+/* ---- receive side after open: keepalives, AllowedIPs, replay window -------
+ * TransportManager.processDecryptedTransport (TransportManager.java:98-119) for a whole
+ * opened batch, on the device: a packet whose status is WG_PKT_OK becomes
+ *   WG_PKT_KEEPALIVE  if len == 0 (:103-105, not forwarded to the tun device);
+ *   WG_PKT_BADIP      if its first nibble is not 4 or 6, or it is shorter than the
+ *                     destination address's end (destinationIPOf, :124-130, throws);
+ *   WG_PKT_FILTERED   if its key slot has an AllowedIPs filter (wg_slot_filters_set) and
+ *                     the destination (bytes 16..19 of IPv4, 24..39 of IPv6) is not in it
+ *                     (destinationFilter.search, :106-108; util/IPFilter.java:49-61);
+ * and stays WG_PKT_OK otherwise (forwarded). Flags: WG_RX_FILTER runs those checks;
+ * WG_RX_REPLAY first applies the key slot's replay window (wg_replay_enable), which the
+ * reference does not have: a packet is WG_PKT_REPLAY if its counter is >= 2^64 - 2^13 - 1,
+ * repeats an earlier WG_PKT_OK packet of the same key slot in this batch, is more than
+ * window_bits behind the highest counter accepted before this batch, or was already
+ * accepted; the window then advances past this batch's accepted counters (the window slides
+ * between batches). Asynchronous on `stream`; run it after wg_open_batch on
+ * the same stream. pt / pt_size: the open's output buffer (plaintexts at out_off).
+ *
+ * wg_filter_set: AllowedIPs filter `filter_id` (< WG_MAX_FILTERS) from n prefixes, exactly as
+ *   IPFilter.insert builds its trie (util/IPFilter.java:30-42), including its search rule:
+ *   a prefix matches an address if the trie walk passes the prefix's node at a depth below
+ *   the address width, so /32 (IPv4) and /128 (IPv6) entries never match - as in the
+ *   reference, whose IPFilter.allowingAll() (0.0.0.0/32, ::/128) lets nothing through.
+ *   Replaces any earlier filter with that id. A key slot without a filter passes every
+ *   destination; a slot mapped to an id never set drops every destination (an empty
+ *   IPFilter, :9-16).
+ * wg_slot_filters_set: filter id per key slot for slots [first_slot, first_slot + n)
+ *   (WG_NO_FILTER: none); the reference keeps one filter per peer (TransportManager.java:44,53).
+ * wg_replay_enable: window of window_bits (a multiple of 64, <= 65536; 0 disables) per key
+ *   slot, all windows empty. wg_keys_set / wg_keys_zero and wg_replay_reset empty the
+ *   windows of the slots they touch (a new key is a new session).
+ * wg_replay_state: a slot's window (top = highest accepted counter + 1, 0 if none; bits =
+ *   window_bits / 64 words, bit (c mod window_bits) set for accepted counter c in the window). */
+#define WG_MAX_FILTERS 65536u
+#define WG_NO_FILTER 0xFFFFFFFFu
+#define WG_RX_FILTER 1u
+#define WG_RX_REPLAY 2u
+typedef struct wg_prefix {
+  uint8_t family;     /* 4 or 6 */
+  uint8_t prefix_len; /* 0..32 or 0..128 */
+  uint8_t addr[16];   /* network byte order; IPv4 in addr[0..3] */
+} wg_prefix;
+int wg_filter_set(wg_ctx* ctx, uint32_t filter_id, const wg_prefix* prefixes, uint32_t n);
+int wg_slot_filters_set(wg_ctx* ctx, uint32_t first_slot, uint32_t n, const uint32_t* filter_ids_host);
+int wg_replay_enable(wg_ctx* ctx, uint32_t window_bits);
+int wg_replay_reset(wg_ctx* ctx, uint32_t first_slot, uint32_t n);
+int wg_replay_state(wg_ctx* ctx, uint32_t slot, uint64_t* top, uint64_t* bits, uint32_t words);
+int wg_rx_check(wg_ctx* ctx, const wg_pkt* desc_dev, uint32_t n, const uint8_t* pt_dev, uint64_t pt_size,
+                uint32_t* status_dev, uint32_t flags, void* stream);
+
 int wg_seal1(wg_ctx* ctx, uint32_t key_slot, uint64_t counter, const uint8_t* pt, uint32_t len, uint8_t* out);
 int wg_open1(wg_ctx* ctx, uint32_t key_slot, uint64_t counter, const uint8_t* in, uint32_t len, uint8_t* pt);
 int wg_batcher_config(wg_ctx* ctx, uint32_t max_batch, uint32_t window_us);

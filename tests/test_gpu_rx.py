@@ -1,0 +1,207 @@
+"""wg_rx_check on the MI355X against oracle/rx.py (pytest -m gpu): keepalives, IP version /
+length, AllowedIPs per key slot (TransportManager.java:98-130, util/IPFilter.java:30-61),
+and the replay window over several batches (window state compared word for word)."""
+import ipaddress
+
+import numpy as np
+import pytest
+
+from oracle import rx
+from wgtest import oracle, splitmix_np, wg
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    import torch
+    assert torch.cuda.is_available()
+    return torch, torch.device("cuda", 0)
+
+
+def _random_prefixes(rng, k):
+    out = []
+    for _ in range(k):
+        if rng.random() < 0.6:
+            a = ipaddress.IPv4Address(int(rng.integers(0, 1 << 32)))
+            p = int(rng.choice([0, 1, 7, 8, 9, 16, 20, 24, 31, 32]))
+        else:
+            a = ipaddress.IPv6Address(int.from_bytes(rng.bytes(16), "big"))
+            p = int(rng.choice([0, 8, 32, 48, 64, 100, 127, 128]))
+        out.append((a, p))
+    return out
+
+
+def _packet(rng, prefixes):
+    """An IP-ish plaintext: mostly v4/v6 with destinations near the filter's prefixes."""
+    kind = rng.random()
+    if kind < 0.05:
+        return b""
+    if kind < 0.10:
+        return bytes([int(rng.choice([0x00, 0x50, 0x85, 0xF0]))]) + rng.bytes(int(rng.integers(0, 60)))
+    v6 = kind > 0.55
+    base, plen = prefixes[int(rng.integers(0, len(prefixes)))] if prefixes else (None, 0)
+    nbytes = 16 if v6 else 4
+    if base is not None and (base.version == 6) == v6 and rng.random() < 0.7:
+        addr = bytearray(base.packed)
+        flip = int(rng.integers(max(plen - 3, 0), nbytes * 8)) if rng.random() < 0.5 else None
+        if flip is not None:
+            addr[flip // 8] ^= 1 << (7 - flip % 8)
+        dst = bytes(addr)
+    else:
+        dst = rng.bytes(nbytes)
+    at = 24 if v6 else 16
+    total = int(rng.integers(at + nbytes - 2, 200)) if rng.random() < 0.1 else int(rng.integers(at + nbytes, 300))
+    p = bytearray(rng.bytes(max(total, 1)))
+    p[0] = (0x60 if v6 else 0x45) | (p[0] & 0x0F)
+    p[at:at + nbytes] = dst[:max(0, min(nbytes, total - at))] if total >= at else b""
+    return bytes(p[:total])
+
+
+def _run(engine, torch, dev, W, slots, counters, pts, status, flags):
+    n = len(pts)
+    lens = np.array([len(p) for p in pts], np.int64)
+    S = ((lens + 15) // 16) * 16 + 16
+    off = np.concatenate([[0], np.cumsum(S)[:-1]]).astype(np.uint64)
+    buf = np.zeros(int(S.sum()), np.uint8)
+    for i, p in enumerate(pts):
+        buf[int(off[i]):int(off[i]) + len(p)] = np.frombuffer(p, np.uint8)
+    desc = W.pack_desc(off, off, counters, lens, slots)
+    d = torch.from_numpy(W.desc_as_int64(desc)).to(dev)
+    st = torch.from_numpy(np.asarray(status, np.int32)).to(dev)
+    engine.rx_check(d, torch.from_numpy(buf).to(dev), st, flags)
+    torch.cuda.synchronize()
+    return st.cpu().numpy().astype(np.int64).tolist()
+
+
+def test_filter_parity_random(engine):
+    torch, dev = _dev()
+    W = wg()
+    rng = np.random.default_rng(7)
+    nf = 6
+    filters = {}
+    for f in range(nf):
+        pre = _random_prefixes(rng, int(rng.integers(0, 12)))
+        if f == 1:
+            pre = [(ipaddress.ip_address("0.0.0.0"), 32), (ipaddress.ip_address("::"), 128)]  # allowingAll()
+        engine.filter_set(f, pre)
+        o = rx.IPFilter()
+        for a, p in pre:
+            o.insert(a.packed, p)
+        filters[f] = (pre, o)
+    # slots 0..9: filter f = slot % 6, slot 7 -> no filter, slot 8 -> an id never set
+    ids = [s % nf for s in range(10)]
+    ids[7] = W._lib.WG_NO_FILTER
+    ids[8] = 4242
+    engine.slot_filters_set(0, ids)
+    n = 20000
+    slots = rng.integers(0, 10, n)
+    pts = []
+    for s in slots:
+        f = ids[int(s)]
+        pts.append(_packet(rng, filters[f][0] if f in filters else []))
+    status = np.where(rng.random(n) < 0.03, 1, 0)
+    got = _run(engine, torch, dev, W, slots, np.arange(n), pts, status, W._lib.WG_RX_FILTER)
+    of = {s: (filters[ids[s]][1] if ids[s] in filters else (rx.IPFilter() if ids[s] != W._lib.WG_NO_FILTER else None))
+          for s in range(10)}
+    want = rx.rx_check(slots, np.arange(n), [len(p) for p in pts], pts, status, of, None)
+    assert got == want
+    kinds = set(want)
+    assert {rx.PKT_OK, rx.PKT_FILTERED, rx.PKT_BADIP, rx.PKT_KEEPALIVE, rx.PKT_BADTAG} <= kinds
+
+
+def test_reference_filter_known_answers_on_device(engine):
+    torch, dev = _dev()
+    W = wg()
+    engine.filter_set(0, [("192.168.1.0", 24), ("2001:db8::", 32)])
+    engine.slot_filters_set(0, [0])
+    pts = []
+    for a in ("192.168.1.55", "192.168.2.1", "2001:db8::abcd", "2001:db9::abcd"):
+        ip = ipaddress.ip_address(a)
+        if ip.version == 4:
+            pts.append(bytes([0x45]) + bytes(15) + ip.packed + bytes(4))
+        else:
+            pts.append(bytes([0x60]) + bytes(23) + ip.packed)
+    got = _run(engine, torch, dev, W, [0] * 4, [0, 1, 2, 3], pts, [0] * 4, W._lib.WG_RX_FILTER)
+    assert got == [rx.PKT_OK, rx.PKT_FILTERED, rx.PKT_OK, rx.PKT_FILTERED]  # IPFilter.java:85-88
+
+
+def test_replay_window_batches_match_oracle(engine):
+    torch, dev = _dev()
+    W = wg()
+    Wb = 256
+    engine.replay_enable(Wb)
+    engine.set_keys(0, splitmix_np(5, 32 * 8).tobytes())  # also empties the windows
+    o = rx.ReplayWindow(Wb)
+    rng = np.random.default_rng(11)
+    base = np.zeros(8, np.int64)
+    for b in range(6):
+        n = 3000
+        slots = rng.integers(0, 8, n)
+        # mostly increasing per slot, with duplicates, stragglers, old replays and jumps
+        c64 = base[slots] + rng.integers(0, 400, n)
+        dup = rng.random(n) < 0.05
+        c64[dup] = np.maximum(c64[dup] - rng.integers(0, 600, dup.sum()), 0)
+        np.maximum.at(base, slots, c64)
+        ctr = c64.astype(np.uint64)
+        if b == 3:  # Reject-After-Messages and beyond
+            ctr[:5] = np.array([rx.REJECT_AFTER - 1 + k for k in range(5)], dtype=np.uint64)
+        status = np.where(rng.random(n) < 0.02, 1, 0)
+        pts = [b""] * n
+        got = _run(engine, torch, dev, W, slots, ctr, pts, status, W._lib.WG_RX_REPLAY)
+        want = o.check_batch(slots, [int(x) for x in ctr], status)
+        assert got == want, b
+        for s in range(8):
+            top, words = engine.replay_state(s, Wb)
+            otop, owords = o.bitmap(s)
+            assert top == otop and [int(x) for x in words] == owords, (b, s)
+    assert any(x == rx.PKT_REPLAY for x in want)
+
+
+def test_replay_then_filter_and_key_reset(engine):
+    """WG_RX_REPLAY | WG_RX_FILTER on opened packets: replay first (keepalives count), then
+    the filter; a new key for a slot empties its window."""
+    torch, dev = _dev()
+    W = wg()
+    O = oracle()
+    engine.replay_enable(128)
+    keys = splitmix_np(9, 32 * 2)
+    engine.set_keys(0, keys.tobytes())
+    engine.filter_set(0, [("10.0.0.0", 8)])
+    engine.slot_filters_set(0, [0, W._lib.WG_NO_FILTER])
+    pts = [bytes([0x45]) + bytes(15) + ipaddress.ip_address(a).packed + bytes(20)
+           for a in ("10.1.2.3", "11.1.2.3", "10.9.9.9")] + [b""]
+    slots = [0, 0, 0, 0]
+    ctrs = [5, 6, 5, 7]
+    lens = np.array([len(p) for p in pts], np.int64)
+    S = ((lens + 16 + 15) // 16) * 16
+    off = np.concatenate([[0], np.cumsum(S)[:-1]]).astype(np.uint64)
+    desc = W.pack_desc(off, off, ctrs, lens, slots)
+    buf = np.zeros(int(S.sum()), np.uint8)
+    for i, p in enumerate(pts):
+        buf[int(off[i]):int(off[i]) + len(p)] = np.frombuffer(p, np.uint8)
+    sealed = np.zeros_like(buf)
+    O.seal_batch(desc, buf, sealed, keys, threads=1)
+    d = torch.from_numpy(W.desc_as_int64(desc)).to(dev)
+    out = torch.zeros(len(buf), dtype=torch.uint8, device=dev)
+    st = torch.zeros(4, dtype=torch.int32, device=dev)
+    engine.open(d, torch.from_numpy(sealed).to(dev), out, st, int(lens.max()))
+    engine.rx_check(d, out, st, W._lib.WG_RX_FILTER | W._lib.WG_RX_REPLAY)
+    torch.cuda.synchronize()
+    assert st.cpu().tolist() == [rx.PKT_OK, rx.PKT_FILTERED, rx.PKT_REPLAY, rx.PKT_KEEPALIVE]
+    assert engine.replay_state(0, 128)[0] == 8
+    engine.set_keys(0, keys[:32].tobytes())
+    assert engine.replay_state(0, 128)[0] == 0
+
+
+def test_rx_argument_contract(engine):
+    torch, dev = _dev()
+    W = wg()
+    lib = W.lib()
+    d = torch.zeros((1, 4), dtype=torch.int64, device=dev)
+    s = torch.zeros(1, dtype=torch.int32, device=dev)
+    b = torch.zeros(64, dtype=torch.uint8, device=dev)
+    E = W._lib.WG_EINVAL
+    assert lib.wg_rx_check(engine.ctx, d.data_ptr(), 1, b.data_ptr(), 64, s.data_ptr(), 0x10, None) == E
+    assert lib.wg_rx_check(engine.ctx, d.data_ptr(), 1, b.data_ptr(), 64, None, 1, None) == E
+    assert lib.wg_replay_enable(engine.ctx, 100) == E
+    assert lib.wg_filter_set(engine.ctx, W._lib.WG_MAX_FILTERS, None, 0) == W._lib.WG_ERANGE

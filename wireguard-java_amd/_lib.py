@@ -23,6 +23,14 @@ WG_ESELFTEST = -74
 WG_PKT_OK = 0
 WG_PKT_BADTAG = 1
 WG_PKT_BADHDR = 2
+WG_PKT_KEEPALIVE = 3
+WG_PKT_BADIP = 4
+WG_PKT_FILTERED = 5
+WG_PKT_REPLAY = 6
+WG_RX_FILTER = 1
+WG_RX_REPLAY = 2
+WG_MAX_FILTERS = 65536
+WG_NO_FILTER = 0xFFFFFFFF
 WG_LEN_INVALID = 0xFFFFFFFF
 WG_TAG_SIZE = 16
 WG_NONCE_SIZE = 12
@@ -56,7 +64,11 @@ class WgAeadDesc(ctypes.Structure):
                 ("ctr0", ctypes.c_uint32), ("nonce", ctypes.c_uint32 * 3), ("_reserved", ctypes.c_uint32 * 3)]
 
 
-assert ctypes.sizeof(WgPkt) == 32 and ctypes.sizeof(WgAeadDesc) == 64
+class WgPrefix(ctypes.Structure):
+    _fields_ = [("family", ctypes.c_uint8), ("prefix_len", ctypes.c_uint8), ("addr", ctypes.c_uint8 * 16)]
+
+
+assert ctypes.sizeof(WgPkt) == 32 and ctypes.sizeof(WgAeadDesc) == 64 and ctypes.sizeof(WgPrefix) == 18
 
 # (name, restype, argtypes) for every symbol include/wgaead.h declares
 _VP, _U32, _U64, _I, _D = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_double
@@ -79,6 +91,12 @@ SIGNATURES = [
     ("wg_frame_seal", _I, [_VP, _VP, _U32, _VP, _VP, _U64, _U64, _U32, _VP]),
     ("wg_parse_open", _I, [_VP, _VP, _U64, _VP, _VP, _VP, _U32, _VP, _VP, _VP]),
     ("wg_aead_batch", _I, [_VP, _I, _VP, _U32, _VP, _U64, _VP, _U64, _VP, _U64, _VP, _U32, _VP]),
+    ("wg_filter_set", _I, [_VP, _U32, _VP, _U32]),
+    ("wg_slot_filters_set", _I, [_VP, _U32, _U32, _VP]),
+    ("wg_replay_enable", _I, [_VP, _U32]),
+    ("wg_replay_reset", _I, [_VP, _U32, _U32]),
+    ("wg_replay_state", _I, [_VP, _U32, ctypes.POINTER(_U64), _VP, _U32]),
+    ("wg_rx_check", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U32, _VP]),
     ("wg_seal1", _I, [_VP, _U32, _U64, _VP, _U32, _VP]),
     ("wg_open1", _I, [_VP, _U32, _U64, _VP, _U32, _VP]),
     ("wg_batcher_config", _I, [_VP, _U32, _U32]),

@@ -9,6 +9,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -75,6 +76,7 @@ struct DevBuf {
 enum Kern { KERN_TRANSPORT = 0, KERN_WAVE1 = 1, KERN_TILE = 2 };
 
 struct Batcher;  // wg_batcher.hip
+struct RxState;  // wg_rx.hip
 
 }  // namespace
 
@@ -98,6 +100,7 @@ struct wg_ctx {
   std::mutex mu;  // serialises host-API calls and plan workspace reuse
   Batcher* batcher = nullptr;
   std::mutex batcher_mu;
+  RxState* rx = nullptr;  // receive-side checks (wg_rx.hip)
   // timing
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
@@ -365,6 +368,7 @@ hipStream_t pick_stream(wg_ctx*, void* stream) { return (hipStream_t)stream; }
 }  // namespace
 
 #include "wg_batcher.hip"
+#include "wg_rx.hip"
 
 extern "C" {
 
@@ -434,6 +438,7 @@ int wg_ctx_destroy(wg_ctx* c) {
   if (!c) return WG_OK;
   batcher_stop(c);
   DeviceGuard g(c->device);
+  rx_free(c);
   if (c->keys) {
     (void)hipMemset(c->keys, 0, (size_t)c->key_slots * 32);  // SymmetricKeypair.clean zeroes keys
     (void)hipDeviceSynchronize();
@@ -472,6 +477,8 @@ int wg_keys_set(wg_ctx* c, uint32_t first, uint32_t n, const uint8_t* keys_host)
   if (!n) return WG_OK;
   DeviceGuard g(c->device);
   HIPTRY(hipMemcpyAsync((uint8_t*)c->keys + (size_t)first * 32, keys_host, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+  int rc;
+  if ((rc = rx_reset_slots(c, first, n, c->stream)) != WG_OK) return rc;  // new key: new session
   HIPTRY(hipStreamSynchronize(c->stream));
   return WG_OK;
 }
@@ -482,6 +489,8 @@ int wg_keys_zero(wg_ctx* c, uint32_t first, uint32_t n) {
   if (!n) return WG_OK;
   DeviceGuard g(c->device);
   HIPTRY(hipMemsetAsync((uint8_t*)c->keys + (size_t)first * 32, 0, (size_t)n * 32, c->stream));
+  int rc;
+  if ((rc = rx_reset_slots(c, first, n, c->stream)) != WG_OK) return rc;
   HIPTRY(hipStreamSynchronize(c->stream));
   return WG_OK;
 }

@@ -1,0 +1,478 @@
+// wg_rx.hip — receive-side checks after open, on the device (included by wg_capi.hip).
+//
+// The reference hands every opened packet to TransportManager.processDecryptedTransport
+// (TransportManager.java:98-119): a zero-length plaintext is a keepalive and is not
+// forwarded (:103-105); otherwise the destination address (destinationIPOf, :124-130:
+// bytes 16..19 of an IPv4 header, 24..39 of an IPv6 header, anything else throws) must
+// be inside the peer's AllowedIPs (IPFilter.search, util/IPFilter.java:49-61) or the
+// packet is dropped (:106-108). wg_rx_check does the same for a whole opened batch and
+// reports the outcome in the status array, after an optional anti-replay window
+// (WG_RX_REPLAY) that the reference does not have.
+//
+// AllowedIPs on the device. IPFilter is a binary trie walked one bit per step; search()
+// reports a match if any node it passes at depths 0 .. nbits-1 ends a subnet, and it
+// stops at the first missing child. Note the depth-nbits node is never tested, so a /32
+// (or /128) entry never matches; IPFilter.allowingAll() inserts exactly such entries
+// (0.0.0.0/32, ::/128) and so matches nothing. The device keeps that behaviour: the
+// binary trie is compiled on the host into stride-8 tables (one 256-entry node per trie
+// node at a depth that is a multiple of 8; entry = next node | "a subnet ended on the
+// way", bit 31), so a lookup is 4 (IPv4) or 16 (IPv6) dependent table reads instead of
+// 32 or 128.
+//
+// Replay window (WG_RX_REPLAY, WireGuard whitepaper §5.4.6 / RFC 6479 style): per key
+// slot, `top` = highest accepted counter + 1 and a ring bitmap of the last W counters.
+// A batch is checked against the window as it stood before the batch:
+//   - counters >= 2^64 - 2^13 - 1 (Reject-After-Messages) are rejected;
+//   - of several authenticated packets with the same (slot, counter) in one batch only
+//     the first (lowest index) can be accepted;
+//   - counter >= top is accepted; top - counter > W is too old; otherwise it is accepted
+//     iff its bit is clear.
+// Then the window advances to the largest accepted counter and records every accepted
+// counter still inside it. The window thus slides between batches: a packet older than
+// W behind an EARLIER packet of the same batch (but not behind the window at the batch's
+// start) is accepted, where a one-packet-at-a-time window would reject it. No counter is
+// ever accepted twice. oracle/rx.py restates these rules one packet at a time.
+#pragma once
+
+namespace {
+
+constexpr uint32_t kRxNoFilter = 0xFFFFFFFFu;
+constexpr uint64_t kRejectAfter = ~0ull - 8191ull - 1ull;  // 2^64 - 2^13 - 1
+constexpr uint64_t kEmptyKey = ~0ull;                      // counters that large are rejected first
+
+struct RxState {
+  // AllowedIPs: host copies of each filter's compiled tables; device image rebuilt on change
+  std::vector<std::vector<uint32_t>> filt_entries;  // per filter: nodes x 256 entries (node 0 = none)
+  std::vector<std::pair<uint32_t, uint32_t>> filt_roots;  // per filter: (root4, root6) node index in its own table
+  DevBuf d_entries, d_hdr, d_slot_filter;
+  bool slot_filter_init = false;
+  // replay window
+  uint32_t window = 0;      // W bits (0: disabled)
+  DevBuf d_top, d_bits;     // per slot: u64 top; W/64 u64 words
+  DevBuf d_newtop, d_hist, d_off, d_tab_key, d_tab_idx, d_scan_tmp;
+};
+
+// ---- host: IPFilter.insert as a binary trie, then stride-8 tables -------------------------
+struct BinTrie {
+  std::vector<std::array<int32_t, 2>> child{{{-1, -1}}};
+  std::vector<uint8_t> end{0};
+  void insert(const uint8_t* addr, uint32_t prefix_len) {  // IPFilter.insert (:30-42)
+    int32_t node = 0;
+    for (uint32_t i = 0; i < prefix_len; ++i) {
+      const int bit = (addr[i / 8] >> (7 - i % 8)) & 1;
+      if (child[node][bit] < 0) {
+        child[node][bit] = (int32_t)child.size();
+        child.push_back({-1, -1});
+        end.push_back(0);
+      }
+      node = child[node][bit];
+    }
+    end[node] = 1;
+  }
+};
+
+// node at depth 8L -> 256 entries; returns its index in `out` (>= 1)
+uint32_t compile_level(const BinTrie& t, int32_t bnode, uint32_t depth, uint32_t nbits, std::vector<uint32_t>& out) {
+  const uint32_t me = (uint32_t)(out.size() / 256);
+  out.resize(out.size() + 256, 0u);
+  for (uint32_t v = 0; v < 256; ++v) {
+    bool found = false, reached = true;
+    int32_t cur = bnode;
+    for (uint32_t k = 0; k < 8; ++k) {  // IPFilter.search (:52-59): test, then descend
+      if (t.end[cur]) found = true;
+      cur = t.child[cur][(v >> (7 - k)) & 1];
+      if (cur < 0) {
+        reached = false;
+        break;
+      }
+    }
+    uint32_t next = 0;
+    if (reached && depth + 8 < nbits) next = compile_level(t, cur, depth + 8, nbits, out);
+    out[(size_t)me * 256 + v] = next | (found ? 0x80000000u : 0u);
+  }
+  return me;
+}
+
+int rx_get(wg_ctx* c, RxState** out) {
+  if (!c->rx) c->rx = new RxState();
+  *out = c->rx;
+  return WG_OK;
+}
+
+void rx_free(wg_ctx* c) {
+  if (!c->rx) return;
+  RxState* r = c->rx;
+  for (DevBuf* b : {&r->d_entries, &r->d_hdr, &r->d_slot_filter, &r->d_top, &r->d_bits, &r->d_newtop, &r->d_hist,
+                    &r->d_off, &r->d_tab_key, &r->d_tab_idx, &r->d_scan_tmp})
+    b->release();
+  delete r;
+  c->rx = nullptr;
+}
+
+// zero the replay window of key slots [first, first + n) (a new key = a new session)
+int rx_reset_slots(wg_ctx* c, uint32_t first, uint32_t n, hipStream_t s) {
+  RxState* r = c->rx;
+  if (!r || !r->window || !n) return WG_OK;
+  HIPTRY(hipMemsetAsync((uint64_t*)r->d_top.p + first, 0, (size_t)n * 8, s));
+  const size_t words = r->window / 64;
+  HIPTRY(hipMemsetAsync((uint64_t*)r->d_bits.p + (size_t)first * words, 0, (size_t)n * words * 8, s));
+  return WG_OK;
+}
+
+}  // namespace
+
+// ---- device -------------------------------------------------------------------------------
+namespace wgrx {
+
+struct RxParams {
+  const wg_pkt* desc;
+  uint32_t n;
+  const uint8_t* pt;
+  uint64_t pt_size;
+  uint32_t* status;
+  uint32_t key_slots;
+  // filter
+  const uint32_t* slot_filter;  // per slot: filter id or kRxNoFilter (NULL: no filters)
+  const uint32_t* hdr;          // per filter: root4, root6 (global node indices)
+  const uint32_t* entries;      // global nodes x 256
+  uint32_t nfilters;
+  // replay
+  uint32_t window;
+  uint64_t* top;
+  uint64_t* bits;
+  uint64_t* newtop;
+  uint32_t* hist;
+  const uint32_t* off;
+  uint64_t* tab_key;
+  uint32_t* tab_idx;
+};
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ bool rp_candidate(const RxParams& P, uint32_t i, uint32_t& slot, uint64_t& ctr) {
+  if (P.status[i] != WG_PKT_OK) return false;
+  const wg_pkt d = P.desc[i];
+  if (d.key_slot >= P.key_slots) return false;
+  slot = d.key_slot;
+  ctr = d.counter;
+  return true;
+}
+
+__global__ void __launch_bounds__(256) k_rp_count(RxParams P) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  uint32_t slot;
+  uint64_t c;
+  if (i < P.n && rp_candidate(P, i, slot, c)) atomicAdd(&P.hist[slot], 1u);
+}
+
+// each slot's packets share a region of 2 x count open-addressing entries keyed by counter;
+// the entry keeps the lowest batch index that carried the counter
+__global__ void __launch_bounds__(256) k_rp_insert(RxParams P) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  uint32_t slot;
+  uint64_t c;
+  if (i >= P.n || !rp_candidate(P, i, slot, c) || c >= kRejectAfter) return;
+  const uint64_t base = 2ull * P.off[slot], size = 2ull * P.hist[slot];
+  uint64_t h = mix64(c) % size;
+  for (uint64_t probe = 0; probe < size; ++probe) {
+    const unsigned long long old =
+        atomicCAS((unsigned long long*)&P.tab_key[base + h], (unsigned long long)kEmptyKey, (unsigned long long)c);
+    if (old == kEmptyKey || old == c) {
+      atomicMin(&P.tab_idx[base + h], i);
+      return;
+    }
+    h = h + 1 == size ? 0 : h + 1;
+  }
+}
+
+__device__ __forceinline__ bool bit_test(const uint64_t* bits, uint32_t W, uint32_t slot, uint64_t c) {
+  const uint64_t pos = c % W;
+  return (bits[(uint64_t)slot * (W / 64) + pos / 64] >> (pos % 64)) & 1ull;
+}
+
+__global__ void __launch_bounds__(256) k_rp_decide(RxParams P) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  uint32_t slot;
+  uint64_t c;
+  if (i >= P.n || !rp_candidate(P, i, slot, c)) return;
+  bool ok = c < kRejectAfter;
+  if (ok) {  // first of its (slot, counter) in the batch?
+    const uint64_t base = 2ull * P.off[slot], size = 2ull * P.hist[slot];
+    uint64_t h = mix64(c) % size;
+    for (uint64_t probe = 0; probe < size; ++probe) {
+      if (P.tab_key[base + h] == c) break;
+      h = h + 1 == size ? 0 : h + 1;
+    }
+    ok = P.tab_idx[base + h] == i;
+  }
+  if (ok) {
+    const uint64_t top = P.top[slot];
+    if (c < top) ok = top - c <= P.window && !bit_test(P.bits, P.window, slot, c);
+  }
+  if (ok) atomicMax((unsigned long long*)&P.newtop[slot], (unsigned long long)(c + 1));
+  else P.status[i] = WG_PKT_REPLAY;
+}
+
+// per slot: the window moves to newtop; ring positions of the counters it passed are cleared
+__global__ void __launch_bounds__(256) k_rp_advance(RxParams P) {
+  const uint32_t slot = blockIdx.x * 256u + threadIdx.x;
+  if (slot >= P.key_slots) return;
+  const uint64_t top = P.top[slot], nt = P.newtop[slot];
+  if (nt <= top) return;
+  const uint32_t W = P.window, words = W / 64;
+  uint64_t* b = P.bits + (uint64_t)slot * words;
+  if (nt - top >= W) {
+    for (uint32_t k = 0; k < words; ++k) b[k] = 0;
+  } else {
+    for (uint64_t x = top; x < nt; ++x) {  // < W positions
+      const uint64_t pos = x % W;
+      b[pos / 64] &= ~(1ull << (pos % 64));
+    }
+  }
+  P.top[slot] = nt;
+}
+
+__global__ void __launch_bounds__(256) k_rp_mark(RxParams P) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  uint32_t slot;
+  uint64_t c;
+  if (i >= P.n || !rp_candidate(P, i, slot, c)) return;  // accepted packets are still OK
+  const uint64_t top = P.top[slot];                       // advanced
+  if (top - c > P.window) return;                         // c < top always here
+  const uint64_t pos = c % P.window;
+  atomicOr((unsigned long long*)&P.bits[(uint64_t)slot * (P.window / 64) + pos / 64], 1ull << (pos % 64));
+}
+
+// keepalive / IP version / AllowedIPs, one thread per packet
+__global__ void __launch_bounds__(256) k_rx_filter(RxParams P) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= P.n || P.status[i] != WG_PKT_OK) return;
+  const wg_pkt d = P.desc[i];
+  if (d.len == 0) {
+    P.status[i] = WG_PKT_KEEPALIVE;
+    return;
+  }
+  if (d.out_off >= P.pt_size || P.pt_size - d.out_off < d.len) {
+    P.status[i] = WG_PKT_BADIP;  // not readable here (open would have rejected it already)
+    return;
+  }
+  const uint8_t* p = P.pt + d.out_off;
+  const uint32_t ver = p[0] >> 4;
+  uint32_t nbytes, at;
+  if (ver == 4) {
+    nbytes = 4;
+    at = 16;
+  } else if (ver == 6) {
+    nbytes = 16;
+    at = 24;
+  } else {
+    P.status[i] = WG_PKT_BADIP;  // destinationIPOf throws IllegalArgumentException
+    return;
+  }
+  if (d.len < at + nbytes) {
+    P.status[i] = WG_PKT_BADIP;  // slice out of bounds
+    return;
+  }
+  if (!P.slot_filter || d.key_slot >= P.key_slots) return;
+  const uint32_t f = P.slot_filter[d.key_slot];
+  if (f == kRxNoFilter) return;
+  uint32_t node = f < P.nfilters ? P.hdr[2 * f + (ver == 6 ? 1 : 0)] : 0u;  // never set: empty filter
+  bool found = false;
+  for (uint32_t L = 0; L < nbytes && node; ++L) {
+    const uint32_t e = P.entries[(size_t)node * 256 + p[at + L]];
+    found |= (e >> 31) != 0;
+    node = e & 0x7FFFFFFFu;
+  }
+  if (!found) P.status[i] = WG_PKT_FILTERED;
+}
+
+}  // namespace wgrx
+
+// ---- C ABI --------------------------------------------------------------------------------
+extern "C" {
+
+int wg_filter_set(wg_ctx* c, uint32_t filter_id, const wg_prefix* prefixes, uint32_t n) {
+  if (!c || (!prefixes && n)) return fail(WG_EINVAL, "NULL argument");
+  if (filter_id >= WG_MAX_FILTERS) return fail(WG_ERANGE, "filter id %u >= %u", filter_id, WG_MAX_FILTERS);
+  BinTrie t4, t6;
+  for (uint32_t k = 0; k < n; ++k) {
+    const wg_prefix& p = prefixes[k];
+    if (p.family == 4 && p.prefix_len <= 32) t4.insert(p.addr, p.prefix_len);
+    else if (p.family == 6 && p.prefix_len <= 128) t6.insert(p.addr, p.prefix_len);
+    else return fail(WG_EINVAL, "prefix %u: family %u / length %u", k, p.family, p.prefix_len);
+  }
+  std::vector<uint32_t> ent(256, 0u);  // node 0: "none"
+  const uint32_t r4 = compile_level(t4, 0, 0, 32, ent);
+  const uint32_t r6 = compile_level(t6, 0, 0, 128, ent);
+  std::lock_guard<std::mutex> lk(c->mu);
+  RxState* r;
+  rx_get(c, &r);
+  if (r->filt_entries.size() <= filter_id) {
+    r->filt_entries.resize(filter_id + 1);
+    r->filt_roots.resize(filter_id + 1, {0u, 0u});
+  }
+  r->filt_entries[filter_id] = std::move(ent);
+  r->filt_roots[filter_id] = {r4, r6};
+  // device image: every filter's nodes back to back, roots rebased
+  std::vector<uint32_t> all, hdr;
+  for (size_t f = 0; f < r->filt_entries.size(); ++f) {
+    const uint32_t base = (uint32_t)(all.size() / 256);
+    const std::vector<uint32_t>& e = r->filt_entries[f];
+    if (e.empty()) {
+      hdr.push_back(0u);
+      hdr.push_back(0u);
+      continue;
+    }
+    for (uint32_t x : e) {
+      const uint32_t nx = x & 0x7FFFFFFFu;
+      all.push_back((x & 0x80000000u) | (nx ? nx + base : 0u));
+    }
+    hdr.push_back(r->filt_roots[f].first + base);
+    hdr.push_back(r->filt_roots[f].second + base);
+  }
+  if (all.size() / 256 >= 0x7FFFFFFFu) return fail(WG_E2BIG, "filter tables too large");
+  DeviceGuard g(c->device);
+  int rc;
+  if ((rc = r->d_entries.ensure(all.size() * 4)) != WG_OK || (rc = r->d_hdr.ensure(hdr.size() * 4)) != WG_OK) return rc;
+  HIPTRY(hipMemcpyAsync(r->d_entries.p, all.data(), all.size() * 4, hipMemcpyHostToDevice, c->stream));
+  HIPTRY(hipMemcpyAsync(r->d_hdr.p, hdr.data(), hdr.size() * 4, hipMemcpyHostToDevice, c->stream));
+  HIPTRY(hipStreamSynchronize(c->stream));
+  return WG_OK;
+}
+
+int wg_slot_filters_set(wg_ctx* c, uint32_t first_slot, uint32_t n, const uint32_t* filter_ids) {
+  if (!c || (!filter_ids && n)) return fail(WG_EINVAL, "NULL argument");
+  if ((uint64_t)first_slot + n > c->key_slots) return fail(WG_ERANGE, "key slots out of range");
+  std::lock_guard<std::mutex> lk(c->mu);
+  RxState* r;
+  rx_get(c, &r);
+  DeviceGuard g(c->device);
+  int rc;
+  if ((rc = r->d_slot_filter.ensure((size_t)c->key_slots * 4)) != WG_OK) return rc;
+  if (!r->slot_filter_init) {
+    HIPTRY(hipMemsetAsync(r->d_slot_filter.p, 0xFF, (size_t)c->key_slots * 4, c->stream));  // no filter
+    r->slot_filter_init = true;
+  }
+  if (n) HIPTRY(hipMemcpyAsync((uint32_t*)r->d_slot_filter.p + first_slot, filter_ids, (size_t)n * 4,
+                               hipMemcpyHostToDevice, c->stream));
+  HIPTRY(hipStreamSynchronize(c->stream));
+  return WG_OK;
+}
+
+int wg_replay_enable(wg_ctx* c, uint32_t window_bits) {
+  if (!c) return fail(WG_EINVAL, "NULL context");
+  if (window_bits && (window_bits % 64 || window_bits > 65536))
+    return fail(WG_EINVAL, "window_bits must be 0 or a multiple of 64 up to 65536");
+  std::lock_guard<std::mutex> lk(c->mu);
+  RxState* r;
+  rx_get(c, &r);
+  DeviceGuard g(c->device);
+  r->window = window_bits;
+  if (!window_bits) return WG_OK;
+  int rc;
+  if ((rc = r->d_top.ensure((size_t)c->key_slots * 8)) != WG_OK ||
+      (rc = r->d_newtop.ensure((size_t)c->key_slots * 8)) != WG_OK ||
+      (rc = r->d_bits.ensure((size_t)c->key_slots * (window_bits / 8))) != WG_OK ||
+      (rc = r->d_hist.ensure(((size_t)c->key_slots + 1) * 4)) != WG_OK ||
+      (rc = r->d_off.ensure(((size_t)c->key_slots + 1) * 4)) != WG_OK)
+    return rc;
+  if ((rc = rx_reset_slots(c, 0, c->key_slots, c->stream)) != WG_OK) return rc;
+  HIPTRY(hipStreamSynchronize(c->stream));
+  return WG_OK;
+}
+
+int wg_replay_reset(wg_ctx* c, uint32_t first_slot, uint32_t n) {
+  if (!c) return fail(WG_EINVAL, "NULL context");
+  if ((uint64_t)first_slot + n > c->key_slots) return fail(WG_ERANGE, "key slots out of range");
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  int rc;
+  if ((rc = rx_reset_slots(c, first_slot, n, c->stream)) != WG_OK) return rc;
+  HIPTRY(hipStreamSynchronize(c->stream));
+  return WG_OK;
+}
+
+int wg_replay_state(wg_ctx* c, uint32_t slot, uint64_t* top, uint64_t* bits, uint32_t words) {
+  if (!c || !top) return fail(WG_EINVAL, "NULL argument");
+  if (slot >= c->key_slots) return fail(WG_ERANGE, "key slot %u", slot);
+  std::lock_guard<std::mutex> lk(c->mu);
+  RxState* r = c->rx;
+  if (!r || !r->window) return fail(WG_EINVAL, "replay window not enabled");
+  if (bits && words != r->window / 64) return fail(WG_EINVAL, "words must be window_bits / 64");
+  DeviceGuard g(c->device);
+  HIPTRY(hipMemcpyAsync(top, (uint64_t*)r->d_top.p + slot, 8, hipMemcpyDeviceToHost, c->stream));
+  if (bits)
+    HIPTRY(hipMemcpyAsync(bits, (uint64_t*)r->d_bits.p + (size_t)slot * words, (size_t)words * 8,
+                          hipMemcpyDeviceToHost, c->stream));
+  HIPTRY(hipStreamSynchronize(c->stream));
+  return WG_OK;
+}
+
+int wg_rx_check(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* pt, uint64_t pt_size, uint32_t* status,
+                uint32_t flags, void* stream) {
+  if (!c) return fail(WG_EINVAL, "NULL context");
+  if (flags & ~(WG_RX_FILTER | WG_RX_REPLAY)) return fail(WG_EINVAL, "unknown rx flags 0x%x", flags);
+  if (n == 0) return WG_OK;
+  if (!desc || !status || (((uintptr_t)desc) & 15u) || (((uintptr_t)status) & 3u))
+    return fail(WG_EINVAL, "descriptor / status arrays must be non-NULL and aligned");
+  if ((flags & WG_RX_FILTER) && !pt) return fail(WG_EINVAL, "NULL plaintext buffer");
+  std::lock_guard<std::mutex> lk(c->mu);
+  RxState* r;
+  rx_get(c, &r);
+  if ((flags & WG_RX_REPLAY) && !r->window) return fail(WG_EINVAL, "WG_RX_REPLAY: call wg_replay_enable first");
+  hipStream_t s = (hipStream_t)stream;
+  DeviceGuard g(c->device);
+  wgrx::RxParams P{};
+  P.desc = desc;
+  P.n = n;
+  P.pt = pt;
+  P.pt_size = pt ? pt_size : 0;
+  P.status = status;
+  P.key_slots = c->key_slots;
+  const uint32_t grid = (n + 255u) / 256u;
+  if (flags & WG_RX_REPLAY) {
+    int rc;
+    if ((rc = r->d_tab_key.ensure((size_t)2 * n * 8)) != WG_OK || (rc = r->d_tab_idx.ensure((size_t)2 * n * 4)) != WG_OK)
+      return rc;
+    size_t tmp = 0;
+    HIPTRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, (uint32_t*)r->d_hist.p, (uint32_t*)r->d_off.p,
+                                            (int)c->key_slots + 1, s));
+    if ((rc = r->d_scan_tmp.ensure(tmp)) != WG_OK) return rc;
+    P.window = r->window;
+    P.top = (uint64_t*)r->d_top.p;
+    P.bits = (uint64_t*)r->d_bits.p;
+    P.newtop = (uint64_t*)r->d_newtop.p;
+    P.hist = (uint32_t*)r->d_hist.p;
+    P.off = (const uint32_t*)r->d_off.p;
+    P.tab_key = (uint64_t*)r->d_tab_key.p;
+    P.tab_idx = (uint32_t*)r->d_tab_idx.p;
+    HIPTRY(hipMemsetAsync(r->d_hist.p, 0, ((size_t)c->key_slots + 1) * 4, s));
+    HIPTRY(hipMemsetAsync(r->d_tab_key.p, 0xFF, (size_t)2 * n * 8, s));
+    HIPTRY(hipMemsetAsync(r->d_tab_idx.p, 0xFF, (size_t)2 * n * 4, s));
+    HIPTRY(hipMemcpyAsync(r->d_newtop.p, r->d_top.p, (size_t)c->key_slots * 8, hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL(wgrx::k_rp_count, dim3(grid), dim3(256), 0, s, P);
+    HIPTRY(hipGetLastError());
+    HIPTRY(hipcub::DeviceScan::ExclusiveSum(r->d_scan_tmp.p, tmp, (uint32_t*)r->d_hist.p, (uint32_t*)r->d_off.p,
+                                            (int)c->key_slots + 1, s));
+    hipLaunchKernelGGL(wgrx::k_rp_insert, dim3(grid), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(wgrx::k_rp_decide, dim3(grid), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(wgrx::k_rp_advance, dim3((c->key_slots + 255u) / 256u), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(wgrx::k_rp_mark, dim3(grid), dim3(256), 0, s, P);
+    HIPTRY(hipGetLastError());
+  }
+  if (flags & WG_RX_FILTER) {
+    P.slot_filter = r->slot_filter_init ? (const uint32_t*)r->d_slot_filter.p : nullptr;
+    P.hdr = (const uint32_t*)r->d_hdr.p;
+    P.entries = (const uint32_t*)r->d_entries.p;
+    P.nfilters = (uint32_t)r->filt_roots.size();
+    hipLaunchKernelGGL(wgrx::k_rx_filter, dim3(grid), dim3(256), 0, s, P);
+    HIPTRY(hipGetLastError());
+  }
+  return WG_OK;
+}
+
+}  // extern "C"

@@ -135,6 +135,44 @@ class Engine:
                                         out.numel(), status.data_ptr(), max_len, L.WG_F_UNIFORM if uniform else 0,
                                         stream if stream is not None else _torch_stream()))
 
+    # ---- receive side after open (wg_rx_check) -------------------------------------
+    def filter_set(self, filter_id: int, prefixes) -> None:
+        """wg_filter_set from (address string or ipaddress object, prefix_len) pairs, as
+        IPFilter.insert(InetAddress, int) takes them (util/IPFilter.java:30-42)."""
+        import ipaddress
+        arr = (L.WgPrefix * max(1, len(prefixes)))()
+        for k, (addr, plen) in enumerate(prefixes):
+            a = ipaddress.ip_address(addr) if isinstance(addr, str) else addr
+            arr[k].family = 4 if a.version == 4 else 6
+            arr[k].prefix_len = plen
+            b = a.packed
+            for i, x in enumerate(b):
+                arr[k].addr[i] = x
+        L.check(self._lib.wg_filter_set(self.ctx, filter_id, ctypes.addressof(arr), len(prefixes)))
+
+    def slot_filters_set(self, first_slot: int, filter_ids) -> None:
+        ids = np.ascontiguousarray(np.asarray(filter_ids, dtype=np.uint32))
+        L.check(self._lib.wg_slot_filters_set(self.ctx, first_slot, len(ids), ids.ctypes.data))
+
+    def replay_enable(self, window_bits: int = 8192) -> None:
+        L.check(self._lib.wg_replay_enable(self.ctx, window_bits))
+
+    def replay_reset(self, first_slot: int, n: int) -> None:
+        L.check(self._lib.wg_replay_reset(self.ctx, first_slot, n))
+
+    def replay_state(self, slot: int, window_bits: int):
+        """(top, bitmap words as uint64 numpy array) of one key slot's window."""
+        top = ctypes.c_uint64()
+        bits = np.zeros(window_bits // 64, np.uint64)
+        L.check(self._lib.wg_replay_state(self.ctx, slot, ctypes.byref(top), bits.ctypes.data, len(bits)))
+        return top.value, bits
+
+    def rx_check(self, desc, pt, status, flags: int = 1, stream: int | None = None) -> None:
+        """wg_rx_check after open(desc, ..., out=pt, status) on the same stream."""
+        n = desc.shape[0]
+        L.check(self._lib.wg_rx_check(self.ctx, desc.data_ptr(), n, pt.data_ptr(), pt.numel(), status.data_ptr(),
+                                      flags, stream if stream is not None else _torch_stream()))
+
     def set_receivers(self, receivers) -> None:
         """wg_ctx_set_receivers: device tensor of receiver_index per key slot for
         seal(..., frame=True) — contiguous, 4-byte integers, on this engine's device, at
