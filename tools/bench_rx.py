@@ -1,0 +1,60 @@
+"""Timing of wg_rx_check on a C1-shaped opened batch (65536 x 1420 B IPv4 plaintexts, one
+key slot with a 3-prefix AllowedIPs filter): filter only, replay only, both. HIP events on
+the launch stream around each of 200 calls; the replay window is re-enabled (emptied,
+untimed) before each call so every call sees fresh counters."""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import importlib
+    import torch
+    W = importlib.import_module("wireguard-java_amd")
+    dev = torch.device("cuda", 0)
+    n, L, S = 65536, 1420, 1440
+    eng = W.Engine(0, key_slots=16)
+    eng.filter_set(0, [("10.0.0.0", 8), ("192.168.0.0", 16), ("2001:db8::", 32)])
+    eng.slot_filters_set(0, [0])
+    pt = np.zeros((n, S), np.uint8)
+    pt[:, 0] = 0x45
+    rng = np.random.default_rng(1)
+    pt[:, 16] = np.where(rng.random(n) < 0.9, 10, 11)
+    pt[:, 17:20] = rng.integers(0, 256, (n, 3))
+    d = torch.from_numpy(W.desc_as_int64(W.pack_desc(np.arange(n) * S, np.arange(n) * S, np.arange(n), L, 0))).to(dev)
+    dpt = torch.from_numpy(pt.reshape(-1)).to(dev)
+    st0 = torch.zeros(n, dtype=torch.int32, device=dev)
+    st = st0.clone()
+    out = {"n": n}
+    for name, flags in (("filter", 1), ("replay", 2), ("filter+replay", 3)):
+        if flags & 2:
+            eng.replay_enable(8192)
+        reps = 200
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(10):
+            st.copy_(st0)
+            eng.rx_check(d, dpt, st, flags)
+        torch.cuda.synchronize()
+        tot = 0.0
+        for _ in range(reps):
+            st.copy_(st0)
+            if flags & 2:
+                eng.replay_enable(8192)  # fresh window (untimed): every counter is new again
+            a.record()
+            eng.rx_check(d, dpt, st, flags)
+            b.record()
+            torch.cuda.synchronize()
+            tot += a.elapsed_time(b)
+        out[name + "_us"] = round(tot / reps * 1e3, 2)
+        out[name + "_status_hist"] = np.bincount(st.cpu().numpy(), minlength=7).tolist()
+    print(json.dumps(out))
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

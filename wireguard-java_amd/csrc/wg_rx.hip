@@ -153,6 +153,39 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
+// Many lanes of a batch usually share a key slot (and a window word): one atomic per distinct
+// key and wave instead of one per lane (65536 same-address atomics serialise at the L2).
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+  return (uint64_t)(uint32_t)__shfl((int)(uint32_t)v, src) | ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), src) << 32);
+}
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  return (uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)v, m) |
+         ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m) << 32);
+}
+// calls f(key, sum, max, or) on the leader lane of every distinct key among active lanes
+// (every lane of the wave must reach this call)
+template <class F>
+__device__ __forceinline__ void wave_group(bool active, uint64_t key, uint64_t val, F f) {
+  const int lane = (int)(threadIdx.x & 63u);
+  for (;;) {
+    const uint64_t act = __ballot(active);
+    if (!act) break;
+    const int leader = __ffsll((unsigned long long)act) - 1;
+    const uint64_t lk = shfl_u64(key, leader);
+    const bool mine = active && key == lk;
+    const uint64_t m = __ballot(mine);
+    uint64_t mx = mine ? val : 0ull, orv = mine ? val : 0ull;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+      const uint64_t a = shfl_xor_u64(mx, o), b = shfl_xor_u64(orv, o);
+      mx = a > mx ? a : mx;
+      orv |= b;
+    }
+    if (lane == leader) f(lk, (uint32_t)__popcll(m), mx, orv);
+    if (mine) active = false;
+  }
+}
+
 __device__ __forceinline__ bool rp_candidate(const RxParams& P, uint32_t i, uint32_t& slot, uint64_t& ctr) {
   if (P.status[i] != WG_PKT_OK) return false;
   const wg_pkt d = P.desc[i];
@@ -164,9 +197,10 @@ __device__ __forceinline__ bool rp_candidate(const RxParams& P, uint32_t i, uint
 
 __global__ void __launch_bounds__(256) k_rp_count(RxParams P) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  uint32_t slot;
-  uint64_t c;
-  if (i < P.n && rp_candidate(P, i, slot, c)) atomicAdd(&P.hist[slot], 1u);
+  uint32_t slot = 0;
+  uint64_t c = 0;
+  const bool act = i < P.n && rp_candidate(P, i, slot, c);
+  wave_group(act, slot, 0ull, [&](uint64_t k, uint32_t cnt, uint64_t, uint64_t) { atomicAdd(&P.hist[k], cnt); });
 }
 
 // each slot's packets share a region of 2 x count open-addressing entries keyed by counter;
@@ -196,11 +230,11 @@ __device__ __forceinline__ bool bit_test(const uint64_t* bits, uint32_t W, uint3
 
 __global__ void __launch_bounds__(256) k_rp_decide(RxParams P) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  uint32_t slot;
-  uint64_t c;
-  if (i >= P.n || !rp_candidate(P, i, slot, c)) return;
-  bool ok = c < kRejectAfter;
-  if (ok) {  // first of its (slot, counter) in the batch?
+  uint32_t slot = 0;
+  uint64_t c = 0;
+  const bool cand = i < P.n && rp_candidate(P, i, slot, c);
+  bool ok = cand && c < kRejectAfter;
+  if (ok) {  // first of its (slot, counter) in the batch? (cand lanes only)
     const uint64_t base = 2ull * P.off[slot], size = 2ull * P.hist[slot];
     uint64_t h = mix64(c) % size;
     for (uint64_t probe = 0; probe < size; ++probe) {
@@ -213,8 +247,10 @@ __global__ void __launch_bounds__(256) k_rp_decide(RxParams P) {
     const uint64_t top = P.top[slot];
     if (c < top) ok = top - c <= P.window && !bit_test(P.bits, P.window, slot, c);
   }
-  if (ok) atomicMax((unsigned long long*)&P.newtop[slot], (unsigned long long)(c + 1));
-  else P.status[i] = WG_PKT_REPLAY;
+  wave_group(ok, slot, c + 1, [&](uint64_t k, uint32_t, uint64_t mx, uint64_t) {
+    atomicMax((unsigned long long*)&P.newtop[k], (unsigned long long)mx);
+  });
+  if (cand && !ok) P.status[i] = WG_PKT_REPLAY;
 }
 
 // per slot: the window moves to newtop; ring positions of the counters it passed are cleared
@@ -227,10 +263,17 @@ __global__ void __launch_bounds__(256) k_rp_advance(RxParams P) {
   uint64_t* b = P.bits + (uint64_t)slot * words;
   if (nt - top >= W) {
     for (uint32_t k = 0; k < words; ++k) b[k] = 0;
-  } else {
-    for (uint64_t x = top; x < nt; ++x) {  // < W positions
-      const uint64_t pos = x % W;
-      b[pos / 64] &= ~(1ull << (pos % 64));
+  } else {  // ring positions [top mod W, +len), as at most two linear ranges, word by word
+    const uint32_t a = (uint32_t)(top % W), len = (uint32_t)(nt - top);
+    const uint32_t r0e = min(a + len, W);
+    const uint32_t ranges[2][2] = {{a, r0e}, {0u, a + len > W ? a + len - W : 0u}};
+    for (int r = 0; r < 2; ++r) {
+      for (uint32_t x = ranges[r][0]; x < ranges[r][1];) {
+        const uint32_t w = x / 64, lo = x % 64, hi = min(64u, ranges[r][1] - w * 64);
+        const uint64_t m = (hi - lo == 64 ? ~0ull : (((1ull << (hi - lo)) - 1ull) << lo));
+        b[w] &= ~m;
+        x = w * 64 + hi;
+      }
     }
   }
   P.top[slot] = nt;
@@ -238,13 +281,15 @@ __global__ void __launch_bounds__(256) k_rp_advance(RxParams P) {
 
 __global__ void __launch_bounds__(256) k_rp_mark(RxParams P) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  uint32_t slot;
-  uint64_t c;
-  if (i >= P.n || !rp_candidate(P, i, slot, c)) return;  // accepted packets are still OK
-  const uint64_t top = P.top[slot];                       // advanced
-  if (top - c > P.window) return;                         // c < top always here
-  const uint64_t pos = c % P.window;
-  atomicOr((unsigned long long*)&P.bits[(uint64_t)slot * (P.window / 64) + pos / 64], 1ull << (pos % 64));
+  uint32_t slot = 0;
+  uint64_t c = 0;
+  bool act = i < P.n && rp_candidate(P, i, slot, c);  // accepted packets are still OK
+  if (act) act = P.top[slot] - c <= P.window;          // top advanced; c < top here
+  const uint64_t pos = act ? c % P.window : 0ull;
+  const uint64_t word = (uint64_t)slot * (P.window / 64) + pos / 64;
+  wave_group(act, word, 1ull << (pos % 64), [&](uint64_t k, uint32_t, uint64_t, uint64_t orv) {
+    atomicOr((unsigned long long*)&P.bits[k], (unsigned long long)orv);
+  });
 }
 
 // keepalive / IP version / AllowedIPs, one thread per packet
