@@ -29,6 +29,17 @@ WG_HOST_PATH=copy timeout -k 10 300 python bench.py --workload c4 --steps 5 --wa
 cat $O/bench_c4_pinned_copy.json
 timeout -k 10 300 python bench.py --workload c4 --host-mem pageable --steps 3 --warmup 1 > $O/bench_c4_pageable.json 2>> $O/bench.err
 cat $O/bench_c4_pageable.json
+echo "[round] host-to-host pipeline (UDP loopback)"
+for k in 1 8; do
+  timeout -k 10 200 ./tools/host_pipeline --backend gpu --packets 65536 --reps 5 --udp-streams $k --tun >> $O/host_pipeline_gpu.jsonl
+done
+timeout -k 10 300 ./tools/host_pipeline --backend cpu --oracle oracle/liboracle.so --threads 16 --packets 65536 --reps 3 --udp-streams 8 --tun >> $O/host_pipeline_cpu.jsonl
+cat $O/host_pipeline_gpu.jsonl $O/host_pipeline_cpu.jsonl
+echo "[round] receive-side checks"; timeout -k 10 120 python tools/bench_rx.py > $O/rx_timing.json; cat $O/rx_timing.json
+echo "[round] per-packet batcher"
+for t in 1 16 64; do timeout -k 10 120 ./tools/batcher_bench $t $((t == 1 ? 2000 : 160000 / t)) 1420 >> $O/batcher.jsonl; done
+timeout -k 10 120 ./tools/batcher_bench 16 10000 0 >> $O/batcher.jsonl
+cat $O/batcher.jsonl
 cd /tmp && export TMPDIR=/tmp
 echo "[round] rocprofv3 stats"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $ROOT/bench.py --no-cpu-baseline > $O/prof_bench.json 2> $O/prof.log

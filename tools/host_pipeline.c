@@ -22,7 +22,8 @@
  * Build: gcc -O2 -pthread -Iinclude -o tools/host_pipeline tools/host_pipeline.c \
  *          -Lwireguard-java_amd -l:libwgaead.so -ldl -Wl,-rpath,'$ORIGIN/../wireguard-java_amd'
  * Run:   tools/host_pipeline [--backend gpu|cpu] [--oracle PATH] [--threads T] [--packets N]
- *                            [--len L] [--reps R] [--tun]   (--tun: try a real tun device)
+ *                            [--len L] [--reps R] [--udp-streams K] [--tun]
+ *        (--tun: try a real tun device; K socket pairs with a sender and a receiver thread each)
  * Output: one JSON line. */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
@@ -195,11 +196,51 @@ static void* rx_loop(void* arg) {
   return NULL;
 }
 
+/* ---- one UDP stripe: a sender thread and a receiver thread on their own socket pair ---- */
+typedef struct {
+  int tx_sock;
+  struct sockaddr_in addr;
+  uint8_t* tx;
+  uint32_t lo, hi, window, L, sent;
+  rx_t R;
+} stripe_t;
+
+static void* tx_loop(void* arg) {
+  stripe_t* S = (stripe_t*)arg;
+  struct mmsghdr msgs[256];
+  struct iovec iov[256];
+  const uint32_t n = S->hi - S->lo;
+  uint32_t sent = 0;
+  double last_progress = now_s();
+  while (sent < n) {
+    const uint32_t inflight = sent - atomic_load(&S->R.received);
+    if (inflight + 256 > S->window) {
+      if (now_s() - last_progress > 0.2) break; /* receiver stalled: datagrams were dropped */
+      continue;
+    }
+    last_progress = now_s();
+    const uint32_t k = n - sent < 256 ? n - sent : 256;
+    for (uint32_t j = 0; j < k; ++j) {
+      iov[j].iov_base = S->tx + (size_t)(S->lo + sent + j) * UDP_STRIDE;
+      iov[j].iov_len = HDR + S->L + 16;
+      memset(&msgs[j].msg_hdr, 0, sizeof msgs[j].msg_hdr);
+      msgs[j].msg_hdr.msg_iov = &iov[j];
+      msgs[j].msg_hdr.msg_iovlen = 1;
+      msgs[j].msg_hdr.msg_name = &S->addr;
+      msgs[j].msg_hdr.msg_namelen = sizeof S->addr;
+    }
+    const int m = sendmmsg(S->tx_sock, msgs, k, 0);
+    if (m > 0) sent += (uint32_t)m;
+  }
+  S->sent = sent;
+  return NULL;
+}
+
 int main(int argc, char** argv) {
   const char* bk = "gpu";
   const char* oracle_path = NULL;
   uint32_t n = 65536, L = 1420, reps = 5;
-  int threads = 16, try_tun = 0;
+  int threads = 16, try_tun = 0, streams = 1;
   for (int i = 1; i < argc; ++i)
     if (!strcmp(argv[i], "--tun")) try_tun = 1;
   for (int i = 1; i + 1 < argc; i += 2) {
@@ -210,8 +251,9 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--packets")) n = (uint32_t)atoi(argv[i + 1]);
     else if (!strcmp(argv[i], "--len")) L = (uint32_t)atoi(argv[i + 1]);
     else if (!strcmp(argv[i], "--reps")) reps = (uint32_t)atoi(argv[i + 1]);
+    else if (!strcmp(argv[i], "--udp-streams")) streams = atoi(argv[i + 1]);
   }
-  if (L < 28 || L > 1420 || n == 0 || reps == 0) {
+  if (L < 28 || L > 1420 || n == 0 || reps == 0 || streams < 1 || streams > 64) {
     fprintf(stderr, "bad arguments\n");
     return 2;
   }
@@ -254,23 +296,33 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < (size_t)n * TUN_STRIDE; ++i) tun[i] = (uint8_t)splitmix(&s);
     for (uint32_t i = 0; i < n; ++i) tun[(size_t)i * TUN_STRIDE] = 0x45;
   }
-  /* loopback UDP pair */
-  int tx_sock = socket(AF_INET, SOCK_DGRAM, 0), rx_sock = socket(AF_INET, SOCK_DGRAM, 0);
-  int big = 64 << 20;
-  setsockopt(rx_sock, SOL_SOCKET, SO_RCVBUF, &big, sizeof big);
-  setsockopt(tx_sock, SOL_SOCKET, SO_SNDBUF, &big, sizeof big);
+  /* loopback UDP: `streams` socket pairs, each with a sender and a receiver thread over its
+   * share of the batch (one flow per socket, as several peers' sessions would be) */
+  stripe_t* SS = calloc((size_t)streams, sizeof(stripe_t));
   int rcvbuf = 0;
-  socklen_t rl = sizeof rcvbuf;
-  getsockopt(rx_sock, SOL_SOCKET, SO_RCVBUF, &rcvbuf, &rl);
-  struct sockaddr_in addr = {0};
-  addr.sin_family = AF_INET;
-  inet_pton(AF_INET, "127.0.0.1", &addr.sin_addr);
-  if (bind(rx_sock, (struct sockaddr*)&addr, sizeof addr) != 0) return 1;
-  socklen_t al = sizeof addr;
-  getsockname(rx_sock, (struct sockaddr*)&addr, &al);
-  /* datagrams in flight at most ~half the receive buffer (loopback UDP drops, not blocks) */
-  uint32_t window = (uint32_t)(rcvbuf / 2 / (int)(UDP_STRIDE + 512));
-  if (window < 16) window = 16;
+  for (int k = 0; k < streams; ++k) {
+    stripe_t* S = &SS[k];
+    S->tx_sock = socket(AF_INET, SOCK_DGRAM, 0);
+    S->R.sock = socket(AF_INET, SOCK_DGRAM, 0);
+    int big = 64 << 20;
+    setsockopt(S->R.sock, SOL_SOCKET, SO_RCVBUF, &big, sizeof big);
+    setsockopt(S->tx_sock, SOL_SOCKET, SO_SNDBUF, &big, sizeof big);
+    socklen_t rl = sizeof rcvbuf;
+    getsockopt(S->R.sock, SOL_SOCKET, SO_RCVBUF, &rcvbuf, &rl);
+    S->addr.sin_family = AF_INET;
+    inet_pton(AF_INET, "127.0.0.1", &S->addr.sin_addr);
+    if (bind(S->R.sock, (struct sockaddr*)&S->addr, sizeof S->addr) != 0) return 1;
+    socklen_t al = sizeof S->addr;
+    getsockname(S->R.sock, (struct sockaddr*)&S->addr, &al);
+    S->lo = (uint32_t)((uint64_t)n * k / streams);
+    S->hi = (uint32_t)((uint64_t)n * (k + 1) / streams);
+    S->L = L;
+    S->tx = tx;
+    /* datagrams in flight at most ~half the receive buffer (loopback UDP drops, not blocks) */
+    S->window = (uint32_t)(rcvbuf / 2 / (int)(UDP_STRIDE + 512));
+    if (S->window < 16) S->window = 16;
+  }
+  const uint32_t window = SS[0].window;
 
   double t_seal = 0, t_xfer = 0, t_open = 0, t_total = 0;
   uint64_t delivered = 0, dropped = 0, bad = 0, mismatched = 0;
@@ -289,51 +341,40 @@ int main(int argc, char** argv) {
       return 1;
     }
     const double b = now_s();
-    rx_t R = {rx_sock, rxr, n, lens, 0, 0};
-    pthread_t th;
-    pthread_create(&th, NULL, rx_loop, &R);
-    struct mmsghdr msgs[256];
-    struct iovec iov[256];
-    uint32_t sent = 0;
-    double last_progress = now_s();
-    while (sent < n) {
-      uint32_t inflight = sent - atomic_load(&R.received);
-      if (inflight + 256 > window) {
-        if (now_s() - last_progress > 0.2) { /* receiver stalled: datagrams were dropped */
-          break;
-        }
-        continue;
-      }
-      last_progress = now_s();
-      uint32_t k = n - sent < 256 ? n - sent : 256;
-      for (uint32_t j = 0; j < k; ++j) {
-        iov[j].iov_base = tx + (size_t)(sent + j) * UDP_STRIDE;
-        iov[j].iov_len = HDR + L + 16;
-        memset(&msgs[j].msg_hdr, 0, sizeof msgs[j].msg_hdr);
-        msgs[j].msg_hdr.msg_iov = &iov[j];
-        msgs[j].msg_hdr.msg_iovlen = 1;
-        msgs[j].msg_hdr.msg_name = &addr;
-        msgs[j].msg_hdr.msg_namelen = sizeof addr;
-      }
-      int m = sendmmsg(tx_sock, msgs, k, 0);
-      if (m > 0) sent += (uint32_t)m;
+    pthread_t rth[64], tth[64];
+    for (int k = 0; k < streams; ++k) {
+      stripe_t* S = &SS[k];
+      S->R.ring = rxr + (size_t)S->lo * UDP_STRIDE;
+      S->R.lens = lens + S->lo;
+      S->R.n = S->hi - S->lo;
+      atomic_store(&S->R.received, 0);
+      atomic_store(&S->R.stop, 0);
+      pthread_create(&rth[k], NULL, rx_loop, &S->R);
+      pthread_create(&tth[k], NULL, tx_loop, S);
     }
+    for (int k = 0; k < streams; ++k) pthread_join(tth[k], NULL);
     const double t_wait = now_s();
-    while (atomic_load(&R.received) < sent && now_s() - t_wait < 0.5) {
+    for (int k = 0; k < streams; ++k) {
+      while (atomic_load(&SS[k].R.received) < SS[k].sent && now_s() - t_wait < 0.5) {
+      }
+      atomic_store(&SS[k].R.stop, 1);
+      pthread_join(rth[k], NULL);
     }
-    atomic_store(&R.stop, 1);
-    pthread_join(th, NULL);
-    const uint32_t got = atomic_load(&R.received);
-    const double c2 = now_s();
     /* open what arrived: header -> counter, descriptor into the received ring */
-    for (uint32_t i = 0; i < got; ++i) {
-      const uint8_t* h = rxr + (size_t)i * UDP_STRIDE;
-      uint64_t cc;
-      memcpy(&cc, h + 8, 8);
-      const uint32_t idx = (uint32_t)(cc - ctr);
-      od[i] = (wg_pkt){(uint64_t)i * UDP_STRIDE + HDR, (uint64_t)(idx < n ? idx : 0) * TUN_STRIDE, cc,
-                       lens[i] >= HDR + 16 ? lens[i] - HDR - 16 : 0, 0};
+    uint32_t got = 0;
+    for (int k = 0; k < streams; ++k) {
+      const uint32_t gk = atomic_load(&SS[k].R.received);
+      for (uint32_t i = 0; i < gk; ++i) {
+        const uint32_t pos = SS[k].lo + i;
+        const uint8_t* h = rxr + (size_t)pos * UDP_STRIDE;
+        uint64_t cc;
+        memcpy(&cc, h + 8, 8);
+        const uint32_t idx = (uint32_t)(cc - ctr);
+        od[got++] = (wg_pkt){(uint64_t)pos * UDP_STRIDE + HDR, (uint64_t)(idx < n ? idx : 0) * TUN_STRIDE, cc,
+                             lens[pos] >= HDR + 16 ? lens[pos] - HDR - 16 : 0, 0};
+      }
     }
+    const double c2 = now_s();
     if (got && do_open(&B, od, got, rxr, (uint64_t)n * UDP_STRIDE, back, (uint64_t)n * TUN_STRIDE, st, L) != 0) {
       fprintf(stderr, "open failed: %s\n", B.gpu ? wg_last_error() : "");
       return 1;
@@ -356,11 +397,11 @@ int main(int argc, char** argv) {
   }
   const double GiB = (double)(1u << 30), per = (double)n * L;
   printf("{\"tool\": \"host_pipeline\", \"backend\": \"%s\", \"threads\": %d, \"packets\": %u, \"len\": %u, "
-         "\"reps\": %u, \"tun\": \"%s\", \"tun_read_gib_s\": %.3f, \"udp_rcvbuf\": %d, \"inflight_window\": %u, "
+         "\"reps\": %u, \"udp_streams\": %d, \"tun\": \"%s\", \"tun_read_gib_s\": %.3f, \"udp_rcvbuf\": %d, \"inflight_window\": %u, "
          "\"seal_gib_s\": %.3f, \"udp_loopback_gib_s\": %.3f, \"open_gib_s\": %.3f, "
          "\"end_to_end_gib_s\": %.3f, \"delivered\": %llu, \"dropped\": %llu, \"bad_tag\": %llu, "
          "\"mismatched\": %llu}\n",
-         bk, B.gpu ? 0 : threads, n, L, reps, g_tun_note, tun_rate, rcvbuf, window, per * reps / t_seal / GiB,
+         bk, B.gpu ? 0 : threads, n, L, reps, streams, g_tun_note, tun_rate, rcvbuf, window, per * reps / t_seal / GiB,
          (double)delivered * L / t_xfer / GiB, (double)delivered * L / t_open / GiB,
          (double)delivered * L / t_total / GiB, (unsigned long long)delivered, (unsigned long long)dropped,
          (unsigned long long)bad, (unsigned long long)mismatched);

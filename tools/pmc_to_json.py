@@ -28,7 +28,7 @@ if stats:
 
 
 def kind(name):
-    if not any(k in name for k in ("k_wave", "k_stream", "k_tile", "k_lean", "k_pipe")):
+    if not any(k in name for k in ("k_transport", "k_wave", "k_stream", "k_tile", "k_lean", "k_pipe")):
         return None
     # template arg 0 = MODE: 0 seal, 1 open
     inner = name.split("<", 1)[1] if "<" in name else ""
