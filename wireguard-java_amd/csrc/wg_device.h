@@ -121,7 +121,7 @@ __device__ __forceinline__ void poly_r_limbs(uint32_t k0, uint32_t k1, uint32_t 
 // carries fit 32 bits) and the wrap carry from d4 is < 2^29.3 (so 5c < 2^32).
 // Each limb's carry seeds the next limb's v_mad_u64_u32 accumulator chain, so a
 // step costs 25 mads + 5 alignbits + 5 ands (+ the 2^130 wrap) and no 64-bit adds.
-#ifndef WG_POLY_ASM
+#ifdef WG_POLY_C  // the plain-C product (the compiler adds each limb's carry with a separate 64-bit add)
 __device__ __forceinline__ void poly_mul(uint32_t h[5], const uint32_t r[5], const uint32_t s[5]) {
   const uint32_t h0 = h[0], h1 = h[1], h2 = h[2], h3 = h[3], h4 = h[4];
   uint64_t d = (uint64_t)h0 * r[0] + (uint64_t)h1 * s[4] + (uint64_t)h2 * s[3] + (uint64_t)h3 * s[2] +
@@ -145,9 +145,10 @@ __device__ __forceinline__ void poly_mul(uint32_t h[5], const uint32_t r[5], con
   h[1] += c;
 }
 #else
-// The same product with each v_mad_u64_u32 as an asm statement, so every limb's chain starts
-// from the previous limb's carry (a 64-bit shift pair) instead of the compiler adding the
-// carry to a separately formed chain (2 extra ops per limb).
+// Default: each v_mad_u64_u32 as an asm statement, so every limb's chain starts from the
+// previous limb's carry instead of the compiler adding the carry to a separately formed
+// chain: -1.4% VALU instructions per k_transport launch (SQ_INSTS_VALU 37.70 M -> 37.18 M on
+// C1), bit-exact.
 __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
   uint64_t d, cc;
   asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(cc) : "v"(a), "v"(b), "v"(c));

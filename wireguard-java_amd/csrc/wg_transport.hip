@@ -22,10 +22,15 @@
 // prefetched one packet ahead (one dword per lane), so a slot never waits on a
 // dependent descriptor load when it starts a packet.
 //
-// IO: 16-byte aligned packets move as dwordx4 (a tail block reads whole 16-B chunks,
-// which never leave the granule of a valid byte, and masks); other alignments read
-// aligned dwords and realign with v_alignbyte, and store through a per-lane LDS stage.
-// Open writes the plaintext in the same pass and zero-fills it again if the tag does
+// IO: a lane's 64 payload bytes are fetched before the ARX rounds with LDS-DMA
+// (global_load_lds, 16 B per lane per instruction) into the wave's chunk-major LDS image,
+// so no registers are held across the rounds; chunks holding a valid byte are read whole
+// (an aligned 16-B read never leaves the granule of its first byte) and masked. Unaligned
+// inputs stage aligned dwords through registers (v_alignbyte). Stores are dwordx4 for
+// 16-B aligned outputs, dword + bytes for 4-B aligned ones, bytes otherwise.
+// Per-slot state (offsets, counter, length, flags, R = r^8, 5R, s, key) lives in a 128-B
+// LDS record. A wave whose 8 slots share one key slot fetches the key through the scalar
+// cache. Open writes the plaintext in the same pass and zero-fills it again if the tag does
 // not verify (the host per-packet wrappers copy back only verified plaintext, as
 // ChaCha20Poly1305.java:40-56 leaves dst untouched).
 #pragma once
@@ -401,8 +406,12 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
         const uint4 rr = rec[s].R0;
         uint32_t y[5];
         poly_r_limbs(rr.x, rr.y, rr.z, rr.w, y);
+#ifndef WG_ABL_NOSCAN
 #pragma unroll
         for (uint32_t st = 1; st < 8u; st <<= 1) {
+#else
+        for (uint32_t st = 8; st < 8u; st <<= 1) {
+#endif
           uint32_t z[5], zs[5];
 #pragma unroll
           for (int i = 0; i < 5; ++i) z[i] = __shfl(y[i], (int)(j >= st ? lane - st : lane), 64);
@@ -478,9 +487,11 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
             acc[3] += len >> 14;
             acc[4] += 1u << 24;
           }
+#ifndef WG_ABL_NOFINISH
           uint32_t Ws[5];
           poly_scale5(W, Ws);
           poly_mul(acc, W, Ws);
+#endif
         }
 #pragma unroll
         for (int i = 0; i < 5; ++i) {  // slot sum (every lane of the slot ends with it)
@@ -495,7 +506,11 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
         if (valid && j == 0) {
           const uint4 sv = rec[s].s;
           uint32_t tag[4];
+#ifndef WG_ABL_NOFINISH
           poly_finish(acc, sv.x, sv.y, sv.z, sv.w, tag);
+#else
+          tag[0] = acc[0] ^ sv.x; tag[1] = acc[1] ^ sv.y; tag[2] = acc[2] ^ sv.z; tag[3] = acc[3] ^ sv.w;
+#endif
           if constexpr (MODE == WG_MODE_SEAL) {
             uint8_t* tp = outp + len;
             if ((((uintptr_t)tp) & 15u) == 0) {

@@ -194,6 +194,70 @@ public final class TransportBatch {
 		}
 	}
 
+	/**
+	 * An AllowedIPs filter from subnets, built as IPFilter.insert builds its trie
+	 * (util/IPFilter.java:30-42) and searched with IPFilter.search's rule on the device.
+	 * {@code filterId} is the peer's; map the peer's receive key slots to it with {@link #mapSlots}.
+	 */
+	public static void setFilter(int filterId, java.net.InetAddress[] subnets, int[] prefixLengths) {
+		if (subnets.length != prefixLengths.length)
+			throw new IllegalArgumentException("one prefix length per subnet");
+		try (var arena = Arena.ofConfined()) {
+			var table = arena.allocate(18L * Math.max(1, subnets.length), 1);  // wg_prefix {u8 family, u8 len, u8 addr[16]}
+			for (int i = 0; i < subnets.length; i++) {
+				byte[] a = subnets[i].getAddress();
+				table.set(JAVA_BYTE, 18L * i, (byte) (a.length == 4 ? 4 : 6));
+				table.set(JAVA_BYTE, 18L * i + 1, (byte) prefixLengths[i]);
+				MemorySegment.copy(MemorySegment.ofArray(a), 0, table, 18L * i + 2, a.length);
+			}
+			WgAead.check((int) WgAead.FILTER_SET.invokeExact(WgAead.CTX, filterId, table, subnets.length));
+		} catch (RuntimeException e) {
+			throw e;
+		} catch (Throwable e) {
+			throw new RuntimeException(e);
+		}
+	}
+
+	/** Filter id per key slot for slots [first, first + ids.length); WgAead.WG_NO_FILTER = pass all. */
+	public static void mapSlots(int firstSlot, int[] ids) {
+		try (var arena = Arena.ofConfined()) {
+			var a = arena.allocate(4L * Math.max(1, ids.length), 4);
+			MemorySegment.copy(MemorySegment.ofArray(ids), 0, a, 0, 4L * ids.length);
+			WgAead.check((int) WgAead.SLOT_FILTERS_SET.invokeExact(WgAead.CTX, firstSlot, ids.length, a));
+		} catch (RuntimeException e) {
+			throw e;
+		} catch (Throwable e) {
+			throw new RuntimeException(e);
+		}
+	}
+
+	/** Per-key-slot replay window of {@code windowBits} (the reference has none); 0 disables. */
+	public static void enableReplayWindow(int windowBits) {
+		try {
+			WgAead.check((int) WgAead.REPLAY_ENABLE.invokeExact(WgAead.CTX, windowBits));
+		} catch (RuntimeException e) {
+			throw e;
+		} catch (Throwable e) {
+			throw new RuntimeException(e);
+		}
+	}
+
+	/**
+	 * processDecryptedTransport for an opened device batch (run after {@link #openDevice} on
+	 * the same stream): status[i] stays WG_PKT_OK (forward to the tun queue) or becomes
+	 * WG_PKT_KEEPALIVE / WG_PKT_BADIP / WG_PKT_FILTERED / WG_PKT_REPLAY (drop).
+	 */
+	public static void rxCheck(MemorySegment table, int n, MemorySegment pt, long ptSize, MemorySegment status,
+	                           int flags, MemorySegment stream) {
+		try {
+			WgAead.check((int) WgAead.RX_CHECK.invokeExact(WgAead.CTX, table, n, pt, ptSize, status, flags, stream));
+		} catch (RuntimeException e) {
+			throw e;
+		} catch (Throwable e) {
+			throw new RuntimeException(e);
+		}
+	}
+
 	public static void sync(MemorySegment stream) {
 		try {
 			WgAead.check((int) WgAead.SYNC.invokeExact(WgAead.CTX, stream));

@@ -27,10 +27,14 @@ public final class WgAead {
 	public static final int WG_MODE_SEAL = 0, WG_MODE_OPEN = 1, WG_MODE_CIPHER = 2, WG_MODE_MAC = 3;
 	public static final int WG_F_UNIFORM = 1;
 	public static final int WG_PKT_OK = 0, WG_PKT_BADTAG = 1, WG_PKT_BADHDR = 2;
+	/** wg_rx_check outcomes (TransportManager.processDecryptedTransport, TransportManager.java:98-119). */
+	public static final int WG_PKT_KEEPALIVE = 3, WG_PKT_BADIP = 4, WG_PKT_FILTERED = 5, WG_PKT_REPLAY = 6;
+	public static final int WG_RX_FILTER = 1, WG_RX_REPLAY = 2, WG_NO_FILTER = -1;
 	public static final long AEAD_DESC_SIZE = 64, PKT_DESC_SIZE = 32;
 
 	static final MethodHandle SELFTEST, CTX_CREATE, LAST_ERROR, KEYS_SET, KEYS_ZERO, SEAL1, OPEN1, AEAD_HOST,
-		SEAL_BATCH, OPEN_BATCH, SYNC, SEAL_HOST, OPEN_HOST, HOST_ALLOC, HOST_FREE, FRAME_SEAL, PARSE_OPEN;
+		SEAL_BATCH, OPEN_BATCH, SYNC, SEAL_HOST, OPEN_HOST, HOST_ALLOC, HOST_FREE, FRAME_SEAL, PARSE_OPEN,
+		FILTER_SET, SLOT_FILTERS_SET, REPLAY_ENABLE, REPLAY_RESET, RX_CHECK;
 
 	/** The process-wide context (one HIP device, its stream and its device key table). */
 	static final MemorySegment CTX;
@@ -68,6 +72,16 @@ public final class WgAead {
 			ADDRESS, JAVA_LONG, ADDRESS, JAVA_LONG, ADDRESS, JAVA_INT, JAVA_INT));
 		HOST_ALLOC = down(linker, symbols, "wg_host_alloc", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_LONG, ADDRESS));
 		HOST_FREE = down(linker, symbols, "wg_host_free", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS));
+		// receive side after open (TransportManager.java:98-130, util/IPFilter.java)
+		FILTER_SET = down(linker, symbols, "wg_filter_set", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT, ADDRESS,
+			JAVA_INT));
+		SLOT_FILTERS_SET = down(linker, symbols, "wg_slot_filters_set", FunctionDescriptor.of(JAVA_INT, ADDRESS,
+			JAVA_INT, JAVA_INT, ADDRESS));
+		REPLAY_ENABLE = down(linker, symbols, "wg_replay_enable", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT));
+		REPLAY_RESET = down(linker, symbols, "wg_replay_reset", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT,
+			JAVA_INT));
+		RX_CHECK = down(linker, symbols, "wg_rx_check", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT,
+			ADDRESS, JAVA_LONG, ADDRESS, JAVA_INT, ADDRESS));
 
 		int device = Integer.getInteger("wg.device", 0);
 		KEY_SLOTS = Integer.getInteger("wg.keySlots", 65536);
