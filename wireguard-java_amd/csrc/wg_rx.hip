@@ -155,16 +155,31 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 
 // Many lanes of a batch usually share a key slot (and a window word): one atomic per distinct
 // key and wave instead of one per lane (65536 same-address atomics serialise at the L2).
+// Reductions over a group use DPP row shifts / broadcasts (no LDS traffic); lane 63 ends
+// with the whole wave's result.
+template <int CTRL, int ROW_MASK, int BANK_MASK>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, BANK_MASK, false);
+}
+template <bool OR>
+__device__ __forceinline__ uint32_t wave_reduce(uint32_t v) {  // max or or over the wave (identity 0)
+  auto op = [](uint32_t a, uint32_t b) { return OR ? (a | b) : (a > b ? a : b); };
+  uint32_t r = op(v, dpp<0x111, 0xf, 0xf>(v));  // row_shr:1
+  r = op(r, dpp<0x112, 0xf, 0xf>(v));           // row_shr:2
+  r = op(r, dpp<0x113, 0xf, 0xf>(v));           // row_shr:3
+  r = op(r, dpp<0x114, 0xf, 0xe>(r));           // row_shr:4, banks 1-3
+  r = op(r, dpp<0x118, 0xf, 0xc>(r));           // row_shr:8, banks 2-3
+  r = op(r, dpp<0x142, 0xa, 0xf>(r));           // row_bcast:15 into rows 1, 3
+  r = op(r, dpp<0x143, 0xc, 0xf>(r));           // row_bcast:31 into rows 2, 3
+  return (uint32_t)__builtin_amdgcn_readlane((int)r, 63);
+}
 __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
-  return (uint64_t)(uint32_t)__shfl((int)(uint32_t)v, src) | ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), src) << 32);
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, src) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), src) << 32);
 }
-__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
-  return (uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)v, m) |
-         ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m) << 32);
-}
-// calls f(key, sum, max, or) on the leader lane of every distinct key among active lanes
-// (every lane of the wave must reach this call)
-template <class F>
+// calls f(key, count, max, or) on the leader lane of every distinct key among active lanes
+// (every lane of the wave must reach this call); MAX / OR select the reductions computed
+template <bool MAX, bool OR, class F>
 __device__ __forceinline__ void wave_group(bool active, uint64_t key, uint64_t val, F f) {
   const int lane = (int)(threadIdx.x & 63u);
   for (;;) {
@@ -174,17 +189,24 @@ __device__ __forceinline__ void wave_group(bool active, uint64_t key, uint64_t v
     const uint64_t lk = shfl_u64(key, leader);
     const bool mine = active && key == lk;
     const uint64_t m = __ballot(mine);
-    uint64_t mx = mine ? val : 0ull, orv = mine ? val : 0ull;
-#pragma unroll
-    for (int o = 32; o; o >>= 1) {
-      const uint64_t a = shfl_xor_u64(mx, o), b = shfl_xor_u64(orv, o);
-      mx = a > mx ? a : mx;
-      orv |= b;
+    uint64_t mx = 0, orv = 0;
+    if constexpr (MAX) {
+      const uint32_t hi = wave_reduce<false>(mine ? (uint32_t)(val >> 32) : 0u);
+      const uint32_t lo = wave_reduce<false>(mine && (uint32_t)(val >> 32) == hi ? (uint32_t)val : 0u);
+      mx = ((uint64_t)hi << 32) | lo;
+    }
+    if constexpr (OR) {
+      const uint32_t hi = wave_reduce<true>(mine ? (uint32_t)(val >> 32) : 0u);
+      const uint32_t lo = wave_reduce<true>(mine ? (uint32_t)val : 0u);
+      orv = ((uint64_t)hi << 32) | lo;
     }
     if (lane == leader) f(lk, (uint32_t)__popcll(m), mx, orv);
     if (mine) active = false;
   }
 }
+
+// open-addressing slot of counter c in a table region of `size` entries (multiply-high)
+__device__ __forceinline__ uint64_t rp_hash(uint64_t c, uint64_t size) { return __umul64hi(mix64(c), size); }
 
 __device__ __forceinline__ bool rp_candidate(const RxParams& P, uint32_t i, uint32_t& slot, uint64_t& ctr) {
   if (P.status[i] != WG_PKT_OK) return false;
@@ -195,12 +217,20 @@ __device__ __forceinline__ bool rp_candidate(const RxParams& P, uint32_t i, uint
   return true;
 }
 
+// also initialises this batch's scratch: the counter table (2n entries) and newtop = top
 __global__ void __launch_bounds__(256) k_rp_count(RxParams P) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i < P.n) {
+    P.tab_key[2ull * i] = kEmptyKey;
+    P.tab_key[2ull * i + 1] = kEmptyKey;
+    P.tab_idx[2ull * i] = ~0u;
+    P.tab_idx[2ull * i + 1] = ~0u;
+  }
+  if (i < P.key_slots) P.newtop[i] = P.top[i];
   uint32_t slot = 0;
   uint64_t c = 0;
   const bool act = i < P.n && rp_candidate(P, i, slot, c);
-  wave_group(act, slot, 0ull, [&](uint64_t k, uint32_t cnt, uint64_t, uint64_t) { atomicAdd(&P.hist[k], cnt); });
+  wave_group<false, false>(act, slot, 0ull, [&](uint64_t k, uint32_t cnt, uint64_t, uint64_t) { atomicAdd(&P.hist[k], cnt); });
 }
 
 // each slot's packets share a region of 2 x count open-addressing entries keyed by counter;
@@ -211,7 +241,7 @@ __global__ void __launch_bounds__(256) k_rp_insert(RxParams P) {
   uint64_t c;
   if (i >= P.n || !rp_candidate(P, i, slot, c) || c >= kRejectAfter) return;
   const uint64_t base = 2ull * P.off[slot], size = 2ull * P.hist[slot];
-  uint64_t h = mix64(c) % size;
+  uint64_t h = rp_hash(c, size);
   for (uint64_t probe = 0; probe < size; ++probe) {
     const unsigned long long old =
         atomicCAS((unsigned long long*)&P.tab_key[base + h], (unsigned long long)kEmptyKey, (unsigned long long)c);
@@ -236,7 +266,7 @@ __global__ void __launch_bounds__(256) k_rp_decide(RxParams P) {
   bool ok = cand && c < kRejectAfter;
   if (ok) {  // first of its (slot, counter) in the batch? (cand lanes only)
     const uint64_t base = 2ull * P.off[slot], size = 2ull * P.hist[slot];
-    uint64_t h = mix64(c) % size;
+    uint64_t h = rp_hash(c, size);
     for (uint64_t probe = 0; probe < size; ++probe) {
       if (P.tab_key[base + h] == c) break;
       h = h + 1 == size ? 0 : h + 1;
@@ -247,7 +277,7 @@ __global__ void __launch_bounds__(256) k_rp_decide(RxParams P) {
     const uint64_t top = P.top[slot];
     if (c < top) ok = top - c <= P.window && !bit_test(P.bits, P.window, slot, c);
   }
-  wave_group(ok, slot, c + 1, [&](uint64_t k, uint32_t, uint64_t mx, uint64_t) {
+  wave_group<true, false>(ok, slot, c + 1, [&](uint64_t k, uint32_t, uint64_t mx, uint64_t) {
     atomicMax((unsigned long long*)&P.newtop[k], (unsigned long long)mx);
   });
   if (cand && !ok) P.status[i] = WG_PKT_REPLAY;
@@ -287,7 +317,7 @@ __global__ void __launch_bounds__(256) k_rp_mark(RxParams P) {
   if (act) act = P.top[slot] - c <= P.window;          // top advanced; c < top here
   const uint64_t pos = act ? c % P.window : 0ull;
   const uint64_t word = (uint64_t)slot * (P.window / 64) + pos / 64;
-  wave_group(act, word, 1ull << (pos % 64), [&](uint64_t k, uint32_t, uint64_t, uint64_t orv) {
+  wave_group<false, true>(act, word, 1ull << (pos % 64), [&](uint64_t k, uint32_t, uint64_t, uint64_t orv) {
     atomicOr((unsigned long long*)&P.bits[k], (unsigned long long)orv);
   });
 }
@@ -496,10 +526,8 @@ int wg_rx_check(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* pt, ui
     P.tab_key = (uint64_t*)r->d_tab_key.p;
     P.tab_idx = (uint32_t*)r->d_tab_idx.p;
     HIPTRY(hipMemsetAsync(r->d_hist.p, 0, ((size_t)c->key_slots + 1) * 4, s));
-    HIPTRY(hipMemsetAsync(r->d_tab_key.p, 0xFF, (size_t)2 * n * 8, s));
-    HIPTRY(hipMemsetAsync(r->d_tab_idx.p, 0xFF, (size_t)2 * n * 4, s));
-    HIPTRY(hipMemcpyAsync(r->d_newtop.p, r->d_top.p, (size_t)c->key_slots * 8, hipMemcpyDeviceToDevice, s));
-    hipLaunchKernelGGL(wgrx::k_rp_count, dim3(grid), dim3(256), 0, s, P);
+    const uint32_t grid_c = (std::max(n, c->key_slots) + 255u) / 256u;
+    hipLaunchKernelGGL(wgrx::k_rp_count, dim3(grid_c), dim3(256), 0, s, P);
     HIPTRY(hipGetLastError());
     HIPTRY(hipcub::DeviceScan::ExclusiveSum(r->d_scan_tmp.p, tmp, (uint32_t*)r->d_hist.p, (uint32_t*)r->d_off.p,
                                             (int)c->key_slots + 1, s));
