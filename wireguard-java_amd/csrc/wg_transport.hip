@@ -386,7 +386,9 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
             uint4 o = make_uint4(x[4 * q] ^ v.x, x[4 * q + 1] ^ v.y, x[4 * q + 2] ^ v.z, x[4 * q + 3] ^ v.w);
             if constexpr (MODE == WG_MODE_SEAL) {
               if (cb < 16u) o = mask_chunk(o, cb);
+#ifndef WG_ABL_NOMACW
               img[64u * q + lane] = o;  // the MAC input is the ciphertext
+#endif
             }
 #ifndef WG_ABL_NOSTORE
             store_chunk(dst + 16u * q, cb, o, oal);
@@ -458,7 +460,11 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
 #pragma unroll
         for (uint32_t t = 0; t < 4u; ++t) {
           if (c0 + 8u * t < c_end) {
+#ifndef WG_ABL_NOPOLYLDS
             uint4 v = ip[2u * t];
+#else
+            uint4 v = make_uint4(acc[0] ^ t, acc[1], acc[2] + c0, acc[3]);
+#endif
             if (c0 + 8u * t == nc) v = make_uint4(0u, 0u, len, 0u);
             poly_mul(acc, R, Rs);
             uint32_t cl[5];
