@@ -326,6 +326,14 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
   // one-packet-per-slot grid would fill more than half the machine, pair packets longest-first
   // (two or more per slot, k_lpt_*): fewer resident waves, but every slot gets a similar share
   if (!(flags & WG_F_UNIFORM) && per_slot < 2 && 2ull * n > cap_slots) per_slot = 2;
+#ifndef WG_PERSISTENT_UNIFORM
+  // uniform lengths: one packet per slot and as many waves as that takes; the hardware
+  // dispatcher starts each new wave as an old one retires, so a wave's packet-start
+  // latency overlaps the other waves' work and the launch walks the rings in order
+  // (C3: 8M packets, +8% over persistent slots; mixed batches stay persistent: one packet
+  // per slot with longest-first order measured 13% slower on C2)
+  if (flags & WG_F_UNIFORM) per_slot = 1;
+#endif
   const uint32_t waves = (uint32_t)((n + 8ull * per_slot - 1) / (8ull * per_slot));
   const uint32_t grid = (waves + wgt::TW - 1) / wgt::TW;
   P.slots = grid * wgt::TW * 8u;
