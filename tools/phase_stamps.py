@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--mode", default="seal", choices=["seal", "open"])
     ap.add_argument("--workload", default="c1", choices=["c1", "c2"])
     ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--keys", type=int, default=256, help="session keys (C1: 1)")
     args = ap.parse_args()
     import torch
     torch.cuda.is_available()
@@ -44,7 +45,7 @@ def main():
     off = np.concatenate([[0], np.cumsum(S)[:-1]]).astype(np.uint64)
     eng = wg.Engine(0, key_slots=256)
     eng.set_keys(0, np.random.default_rng(2).integers(0, 256, 32 * 256, dtype=np.uint8).tobytes())
-    desc = wg.pack_desc(off, off, np.arange(n, dtype=np.uint64), lengths, np.arange(n) % 256)
+    desc = wg.pack_desc(off, off, np.arange(n, dtype=np.uint64), lengths, np.arange(n) % args.keys)
     dev = torch.device("cuda", 0)
     d = torch.from_numpy(wg.desc_as_int64(desc)).to(dev)
     total = int(S.sum())

@@ -1,4 +1,4 @@
-// wg_kernels.h — launch parameters shared by wg_kernels.hip and wg_capi.hip.
+// wg_kernels.h — launch parameters shared by the kernels (wg_tile.hip, wg_wave_r1.hip) and wg_capi.hip.
 #pragma once
 #include <stdint.h>
 
@@ -42,7 +42,7 @@ __global__ void k_plan_tiles(const uint32_t* prefix, uint32_t n, uint32_t C, uin
 
 // LDS bytes of the per-packet records of a tile holding up to `mp` packets
 // (128-byte record + 4-byte first-block index each, plus one); the payload
-// image follows, 16-byte aligned (see tile_rec in wg_kernels.hip).
+// image follows, 16-byte aligned (see tile_rec in wg_tile.hip).
 __host__ __device__ inline uint32_t tile_header_bytes(uint32_t mp) {
   uint32_t b = 128u * mp + 4u * (mp + 1);
   return (b + 15u) & ~15u;
