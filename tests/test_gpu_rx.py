@@ -204,4 +204,8 @@ def test_rx_argument_contract(engine):
     assert lib.wg_rx_check(engine.ctx, d.data_ptr(), 1, b.data_ptr(), 64, s.data_ptr(), 0x10, None) == E
     assert lib.wg_rx_check(engine.ctx, d.data_ptr(), 1, b.data_ptr(), 64, None, 1, None) == E
     assert lib.wg_replay_enable(engine.ctx, 100) == E
+    assert lib.wg_replay_enable(engine.ctx, 0) == 0  # disabled: WG_RX_REPLAY is refused
+    assert lib.wg_rx_check(engine.ctx, d.data_ptr(), 1, b.data_ptr(), 64, s.data_ptr(), 2, None) == E
+    assert lib.wg_rx_check(engine.ctx, d.data_ptr(), 0, None, 0, None, 3, None) == 0  # n = 0
+    assert lib.wg_slot_filters_set(engine.ctx, engine.key_slots, 1, None) == E  # NULL ids with n > 0
     assert lib.wg_filter_set(engine.ctx, W._lib.WG_MAX_FILTERS, None, 0) == W._lib.WG_ERANGE

@@ -411,6 +411,8 @@ int wg_filter_set(wg_ctx* c, uint32_t filter_id, const wg_prefix* prefixes, uint
   }
   if (all.size() / 256 >= 0x7FFFFFFFu) return fail(WG_E2BIG, "filter tables too large");
   DeviceGuard g(c->device);
+  // the tables may be reallocated: no wg_rx_check launched earlier (on any stream) may still read them
+  HIPTRY(hipDeviceSynchronize());
   int rc;
   if ((rc = r->d_entries.ensure(all.size() * 4)) != WG_OK || (rc = r->d_hdr.ensure(hdr.size() * 4)) != WG_OK) return rc;
   HIPTRY(hipMemcpyAsync(r->d_entries.p, all.data(), all.size() * 4, hipMemcpyHostToDevice, c->stream));
@@ -427,6 +429,7 @@ int wg_slot_filters_set(wg_ctx* c, uint32_t first_slot, uint32_t n, const uint32
   rx_get(c, &r);
   DeviceGuard g(c->device);
   int rc;
+  if (!r->slot_filter_init) HIPTRY(hipDeviceSynchronize());  // first use allocates the table
   if ((rc = r->d_slot_filter.ensure((size_t)c->key_slots * 4)) != WG_OK) return rc;
   if (!r->slot_filter_init) {
     HIPTRY(hipMemsetAsync(r->d_slot_filter.p, 0xFF, (size_t)c->key_slots * 4, c->stream));  // no filter
@@ -446,6 +449,7 @@ int wg_replay_enable(wg_ctx* c, uint32_t window_bits) {
   RxState* r;
   rx_get(c, &r);
   DeviceGuard g(c->device);
+  HIPTRY(hipDeviceSynchronize());  // window state may be reallocated under earlier wg_rx_check launches
   r->window = window_bits;
   if (!window_bits) return WG_OK;
   int rc;
