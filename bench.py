@@ -134,29 +134,38 @@ def cpu_baseline(lengths, slots, counters, keys, budget_s: float = 1.5):
             "single_thread_open": round(s_open, 3)}
 
 
-def pmc_valu_insts():
-    """SQ_INSTS_VALU per transport-kernel launch (mean of seal and open) from the committed PMC summary."""
+def pmc_valu_insts(mode="serial"):
+    """SQ_INSTS_VALU per transport-kernel launch from the committed PMC summary: the mean of the seal
+    and open launches (serial steps), or the k_duplex launch (duplex steps; seal + open when the
+    summary has no duplex entry)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
     if not files:
         return None
     try:
         d = json.load(open(files[-1]))
+        if mode == "duplex" and "duplex" in d:
+            return d["duplex"]["counters_mean"]["SQ_INSTS_VALU"]
         v = [d[k]["counters_mean"]["SQ_INSTS_VALU"] for k in ("seal", "open") if k in d]
-        return sum(v) / len(v) if v else None
+        return (sum(v) if mode == "duplex" else sum(v) / len(v)) if len(v) == 2 else None
     except Exception:
         return None
 
 
-def pmc_traffic():
-    """Per-launch HBM bytes of the transport kernel (mean of the seal and open launches) from the
-    newest committed PMC summary (profiles/pmc_*.json, written by tools/pmc_to_json.py)."""
+def pmc_traffic(mode="serial"):
+    """Per-launch HBM bytes of the transport kernel (mean of the seal and open launches, or the
+    k_duplex launch) from the newest committed PMC summary (profiles/pmc_*.json, written by
+    tools/pmc_to_json.py)."""
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
     if not files:
         return None
     try:
         d = json.load(open(files[-1]))
+        if mode == "duplex" and "duplex_hbm_bytes_per_launch" in d:
+            return round(d["duplex_hbm_bytes_per_launch"])
         v = [d[k] for k in ("seal_hbm_bytes_per_launch", "open_hbm_bytes_per_launch") if k in d]
-        return round(sum(v) / len(v)) if v else None
+        if len(v) != 2:
+            return None
+        return round(sum(v)) if mode == "duplex" else round(sum(v) / 2)
     except Exception:
         return None
 
@@ -278,6 +287,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-mem", default="pinned", choices=["pinned", "pageable"])
     ap.add_argument("--streams", type=int, default=1)
+    # duplex: each step is ONE wg_duplex_batch launch that seals this step's batch and opens
+    # the previous step's ciphertext (double-buffered); serial: a seal launch, then an open
+    # launch of the same batch
+    ap.add_argument("--mode", default="serial", choices=["serial", "duplex"])
     ap.add_argument("--kernel", default="default", help="transport kernel (wg_ctx_set_kernel): default|wave1|tile")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -333,7 +346,17 @@ def main():
     main_stream = torch.cuda.current_stream()
     side = [main_stream] if K == 1 else [torch.cuda.Stream(device=dev) for _ in range(K)]
 
+    cts = [ct, torch.zeros_like(ct)] if args.mode == "duplex" else [ct]
+    k_step = [0]
+
+    def step_duplex():
+        k = k_step[0]
+        k_step[0] += 1
+        eng.duplex(d_desc, pt, cts[k & 1], max_len, d_desc, cts[(k + 1) & 1], back, status, max_len, uniform=uniform)
+
     def step():
+        if args.mode == "duplex":
+            return step_duplex()
         for i in range(K):
             a, b = cuts[i], cuts[i + 1]
             with torch.cuda.stream(side[i]):
@@ -350,6 +373,10 @@ def main():
             for s_ in side:
                 main_stream.wait_stream(s_)
 
+    if args.mode == "duplex":
+        if K != 1:
+            raise SystemExit("--mode duplex uses one stream")
+        eng.seal(d_desc, pt, cts[1], max_len, uniform=uniform)  # the first step opens this
     fork()
     t_ramp = time.perf_counter()
     ramp_steps = 0
@@ -379,7 +406,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
-    gpu_step_ms = ev0.elapsed_time(ev1) / args.steps  # = t_seal + t_open (back-to-back launches)
+    gpu_step_ms = ev0.elapsed_time(ev1) / args.steps  # = t_seal + t_open (back-to-back launches), or t_duplex
 
     # per-kernel split (not in the timed region): seal-only and open-only launch trains
     def train(fn, k=10):
@@ -420,9 +447,14 @@ def main():
     # seal reads L, writes L+16; open reads L+16, writes L -> 4L+32 per packet
     step_alg = float((4 * lengths + 32).sum())
     achieved = step_alg / (gpu_step_ms * 1e-3) / 1e9
-    traffic = pmc_traffic() if args.workload == "c1" else None
-    valu = pmc_valu_insts() if args.workload == "c1" else None
+    traffic = pmc_traffic(args.mode) if args.workload == "c1" else None
+    valu = pmc_valu_insts(args.mode) if args.workload == "c1" else None
 
+    launches = 1 if args.mode == "duplex" else 2  # kernel launches per step
+    if args.mode == "duplex":
+        kname = "k_duplex (seal + open halves)"
+    else:
+        kname = "k_transport<SEAL|OPEN>" if args.kernel == "default" else args.kernel
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -438,17 +470,17 @@ def main():
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (random payload in HBM, splitmix64 keys, sequential counters)",
-            "config": {"workload": wdesc, "packets_per_gpu": n, "payload_bytes": int(lengths.mean()),
+            "config": {"workload": wdesc, "packets_per_gpu": n, "payload_bytes": int(lengths.mean()), "step": args.mode,
                        "sessions_per_gpu": nkeys, "parallelism": f"dp{world} sharded by session, no collective"},
-            "roofline": {"bound": "hbm", "kernel": "k_transport<SEAL|OPEN>" if args.kernel == "default" else args.kernel, "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "alg_bytes_per_launch": int(step_alg / 2),
-                         "kernel_ms": round(gpu_step_ms / 2, 5), "seal_ms": round(seal_ms, 5),
+                         "traffic": traffic, "alg_bytes_per_launch": int(step_alg / launches),
+                         "kernel_ms": round(gpu_step_ms / launches, 5), "seal_ms": round(seal_ms, 5),
                          "open_ms": round(open_ms, 5)},
             "verified": all_ok,
         }
         if valu:
-            rate = valu / (gpu_step_ms / 2 * 1e-3)
+            rate = valu / (gpu_step_ms / launches * 1e-3)
             line["valu_roofline"] = {"insts_per_launch": round(valu), "achieved": round(rate / 1e12, 4),
                                      "peak": round(VALU_PEAK_WIPS / 1e12, 4), "unit": "T wave-instr/s",
                                      "frac": round(rate / VALU_PEAK_WIPS, 4), "source": "SQ_INSTS_VALU, profiles/pmc_*.json"}

@@ -153,6 +153,31 @@ int wg_open_batch(wg_ctx* ctx, const wg_pkt* desc_dev, uint32_t n, const uint8_t
                   uint8_t* out_dev, uint64_t out_size, uint32_t* status_dev, uint32_t max_len, uint32_t flags,
                   void* stream);
 
+/* ---- both directions in one launch (device pointers) ----------------------
+ * A node seals its outgoing batch and opens its incoming batch at the same time: the
+ * reference runs both on one ForkJoinPool (TransportManager.java:41 outgoing cipher,
+ * :79 incoming decipher). wg_duplex_batch(seal, open) computes exactly what
+ * wg_seal_batch(seal...) and wg_open_batch(open...) compute, in ONE kernel launch whose
+ * workgroups alternate between the two batches, so neither batch's launch start and tail
+ * leaves the device idle. The two batches run concurrently: the open batch must not read
+ * bytes the seal batch writes in the same call (open the previous call's ciphertext).
+ * seal->flags: WG_F_UNIFORM, WG_F_FRAME (as wg_seal_batch); seal->status is ignored.
+ * open->flags: WG_F_UNIFORM; open->status is required when open->n > 0.
+ * Either n may be 0. */
+typedef struct wg_batch {
+  const wg_pkt* desc; /* device, 16-byte aligned */
+  const uint8_t* in;
+  uint8_t* out;
+  uint32_t* status;   /* open: WG_PKT_* per packet */
+  uint64_t in_size;
+  uint64_t out_size;
+  uint32_t n;
+  uint32_t max_len;
+  uint32_t flags;
+  uint32_t _reserved;
+} wg_batch;
+int wg_duplex_batch(wg_ctx* ctx, const wg_batch* seal, const wg_batch* open, void* stream);
+
 /* ---- general AEAD + primitives (device pointers) --------------------------
  * WG_MODE_SEAL / WG_MODE_OPEN: ChaCha20Poly1305.poly1305AeadEncrypt / Decrypt
  *   with optional AAD and explicit nonce (ChaCha20Poly1305.java:31-60).

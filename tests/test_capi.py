@@ -39,13 +39,16 @@ def test_struct_layout_matches_header(tmp_path):
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "wgaead.h"\n'
                    'int main(void){printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(wg_pkt), offsetof(wg_pkt, len),'
                    ' offsetof(wg_pkt, key_slot), sizeof(wg_aead_desc), offsetof(wg_aead_desc, nonce),'
-                   ' offsetof(wg_aead_desc, ctr0)); return 0;}\n')
+                   ' offsetof(wg_aead_desc, ctr0));'
+                   ' printf("%zu %zu %zu %zu %zu\\n", sizeof(wg_batch), offsetof(wg_batch, status),'
+                   ' offsetof(wg_batch, in_size), offsetof(wg_batch, n), offsetof(wg_batch, flags)); return 0;}\n')
     exe = tmp_path / "layout"
     subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)])
     got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
     L = wg()._lib
     assert got == [ctypes.sizeof(L.WgPkt), L.WgPkt.len.offset, L.WgPkt.key_slot.offset, ctypes.sizeof(L.WgAeadDesc),
-                   L.WgAeadDesc.nonce.offset, L.WgAeadDesc.ctr0.offset]
+                   L.WgAeadDesc.nonce.offset, L.WgAeadDesc.ctr0.offset, ctypes.sizeof(L.WgBatch),
+                   L.WgBatch.status.offset, L.WgBatch.in_size.offset, L.WgBatch.n.offset, L.WgBatch.flags.offset]
     assert wg().WG_PKT_DTYPE.itemsize == 32
 
 

@@ -68,6 +68,15 @@ class WgPrefix(ctypes.Structure):
     _fields_ = [("family", ctypes.c_uint8), ("prefix_len", ctypes.c_uint8), ("addr", ctypes.c_uint8 * 16)]
 
 
+class WgBatch(ctypes.Structure):
+    """wg_batch: one direction of wg_duplex_batch (device pointers)."""
+    _fields_ = [("desc", ctypes.c_void_p), ("in_", ctypes.c_void_p), ("out", ctypes.c_void_p),
+                ("status", ctypes.c_void_p), ("in_size", ctypes.c_uint64), ("out_size", ctypes.c_uint64),
+                ("n", ctypes.c_uint32), ("max_len", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("_reserved", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(WgBatch) == 64
 assert ctypes.sizeof(WgPkt) == 32 and ctypes.sizeof(WgAeadDesc) == 64 and ctypes.sizeof(WgPrefix) == 18
 
 # (name, restype, argtypes) for every symbol include/wgaead.h declares
@@ -87,6 +96,7 @@ SIGNATURES = [
     ("wg_keys_zero", _I, [_VP, _U32, _U32]),
     ("wg_seal_batch", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _U32, _U32, _VP]),
     ("wg_open_batch", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _VP, _U32, _U32, _VP]),
+    ("wg_duplex_batch", _I, [_VP, ctypes.POINTER(WgBatch), ctypes.POINTER(WgBatch), _VP]),
     ("wg_ctx_set_receivers", _I, [_VP, _VP, _U32]),
     ("wg_frame_seal", _I, [_VP, _VP, _U32, _VP, _VP, _U64, _U64, _U32, _VP]),
     ("wg_parse_open", _I, [_VP, _VP, _U64, _VP, _VP, _VP, _U32, _VP, _VP, _VP]),

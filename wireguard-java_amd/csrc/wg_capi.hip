@@ -94,6 +94,7 @@ struct wg_ctx {
   uint32_t resident_waves[2] = {0, 0};    // k_transport<SEAL/OPEN> waves resident at once (occupancy)
   // plan workspace: k_tile block scan, k_transport longest-first order
   DevBuf plan_nb, plan_prefix, plan_tiles, plan_ntiles, plan_tmp, lpt_hist, lpt_order;
+  DevBuf lpt_hist2, lpt_order2;  // the open half of a wg_duplex_batch
   int kern = KERN_TRANSPORT;
   // host-API staging
   DevBuf h_desc, h_in, h_out, h_aad, h_status, h_keys;
@@ -273,6 +274,75 @@ int launch_tiles(wg_ctx* c, const void* desc, uint32_t n, const uint8_t* in, uin
   return ws_release(c, s);
 }
 
+// Parameters and grid of one k_transport direction (shared by k_transport and k_duplex):
+// persistent slots for mixed lengths (longest-first order in lpt_order), one packet per
+// slot for uniform batches. cap_slots: the slots resident at once for this direction.
+template <int MODE>
+int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, uint64_t in_size, uint8_t* out,
+                   uint64_t out_size, uint32_t* status, uint32_t max_len, uint32_t flags, hipStream_t s,
+                   uint64_t cap_slots, DevBuf& lpt_hist, DevBuf& lpt_order, wgt::TransportParams* Pout,
+                   uint32_t* grid_out, bool* ordered_out) {
+  bool ordered = false;
+  wgt::TransportParams P{};
+  P.desc = desc;
+  P.n = n;
+  P.max_len = max_len;
+  P.key_slots = c->key_slots;
+  P.in = in;
+  P.in_size = in_size;
+  P.out = out;
+  P.out_size = out_size;
+  P.keys = c->keys;
+  P.status = status;
+#ifdef WG_DIAG
+  P.stamps = g_stamps;
+#endif
+  uint64_t per_slot = (n + cap_slots - 1) / cap_slots;
+  // mixed lengths: a slot holding one packet runs as long as the longest packet, so once a
+  // one-packet-per-slot grid would fill more than half the machine, pair packets longest-first
+  // (two or more per slot, k_lpt_*): fewer resident waves, but every slot gets a similar share
+  if (!(flags & WG_F_UNIFORM) && per_slot < 2 && 2ull * n > cap_slots) per_slot = 2;
+#ifndef WG_PERSISTENT_UNIFORM
+  // uniform lengths: one packet per slot and as many waves as that takes; the hardware
+  // dispatcher starts each new wave as an old one retires, so a wave's packet-start
+  // latency overlaps the other waves' work and the launch walks the rings in order
+  // (C3: 8M packets, +8% over persistent slots; mixed batches stay persistent: one packet
+  // per slot with longest-first order measured 13% slower on C2)
+  if (flags & WG_F_UNIFORM) per_slot = 1;
+#endif
+  const uint32_t waves = (uint32_t)((n + 8ull * per_slot - 1) / (8ull * per_slot));
+  const uint32_t grid = (waves + wgt::TW - 1) / wgt::TW;
+  P.slots = grid * wgt::TW * 8u;
+  // rounds a slot runs, spread over the 4 issue-priority levels (k_transport)
+  const uint32_t max_rounds = (host_pkt_blocks<WG_MODE_SEAL>(max_len) + 7u) / 8u;
+#ifndef WG_PRIO
+  P.prio_step = 0;
+#else
+  P.prio_step = std::max<uint32_t>(1u, (uint32_t)((per_slot * max_rounds + 3u) / 4u));
+#endif
+  if (!(flags & WG_F_UNIFORM) && per_slot > 1) {  // longest-first order (LPT) for the snake
+    int rc;
+    if ((rc = lpt_hist.ensure(sizeof(uint32_t) * 2 * wgt::LPT_BINS)) != WG_OK) return rc;
+    if ((rc = lpt_order.ensure(sizeof(uint32_t) * (size_t)n)) != WG_OK) return rc;
+    if ((rc = ws_acquire(c, s)) != WG_OK) return rc;
+    uint32_t* hist = (uint32_t*)lpt_hist.p;
+    uint32_t* cursor = hist + wgt::LPT_BINS;
+    HIPTRY(hipMemsetAsync(hist, 0, sizeof(uint32_t) * wgt::LPT_BINS, s));
+    const uint32_t hgrid = std::min<uint32_t>((n + 255u) / 256u, 1024u);
+    hipLaunchKernelGGL((wgt::k_lpt_hist<MODE>), dim3(hgrid), dim3(256), 0, s, desc, n, max_len, hist);
+    hipLaunchKernelGGL(wgt::k_lpt_offsets, dim3(1), dim3(256), 0, s, (const uint32_t*)hist, cursor);
+    hipLaunchKernelGGL((wgt::k_lpt_scatter<MODE>), dim3((n + 255u) / 256u), dim3(256), 0, s, desc, n, max_len, cursor,
+                       (uint32_t*)lpt_order.p);
+    HIPTRY(hipGetLastError());
+    P.order = (const uint32_t*)lpt_order.p;
+    ordered = true;
+  }
+  *Pout = P;
+  *grid_out = grid;
+  *ordered_out = ordered;
+  return WG_OK;
+}
+
 // Transport seal/open through k_transport: persistent slots, 8 per wave. Each slot takes
 // ceil(n / resident slots) packets; mixed-length batches are ordered longest-first on
 // the device first (k_lpt_*), so the slots' snake over the order balances their rounds.
@@ -307,61 +377,12 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
     return WG_OK;
   }
   wgt::TransportParams P{};
-  P.desc = desc;
-  P.n = n;
-  P.max_len = max_len;
-  P.key_slots = c->key_slots;
-  P.in = in;
-  P.in_size = in_size;
-  P.out = out;
-  P.out_size = out_size;
-  P.keys = c->keys;
-  P.status = status;
-#ifdef WG_DIAG
-  P.stamps = g_stamps;
-#endif
-  const uint64_t cap_slots = 8ull * std::max<uint32_t>(c->resident_waves[MODE == WG_MODE_OPEN], wgt::TW);
-  uint64_t per_slot = (n + cap_slots - 1) / cap_slots;
-  // mixed lengths: a slot holding one packet runs as long as the longest packet, so once a
-  // one-packet-per-slot grid would fill more than half the machine, pair packets longest-first
-  // (two or more per slot, k_lpt_*): fewer resident waves, but every slot gets a similar share
-  if (!(flags & WG_F_UNIFORM) && per_slot < 2 && 2ull * n > cap_slots) per_slot = 2;
-#ifndef WG_PERSISTENT_UNIFORM
-  // uniform lengths: one packet per slot and as many waves as that takes; the hardware
-  // dispatcher starts each new wave as an old one retires, so a wave's packet-start
-  // latency overlaps the other waves' work and the launch walks the rings in order
-  // (C3: 8M packets, +8% over persistent slots; mixed batches stay persistent: one packet
-  // per slot with longest-first order measured 13% slower on C2)
-  if (flags & WG_F_UNIFORM) per_slot = 1;
-#endif
-  const uint32_t waves = (uint32_t)((n + 8ull * per_slot - 1) / (8ull * per_slot));
-  const uint32_t grid = (waves + wgt::TW - 1) / wgt::TW;
-  P.slots = grid * wgt::TW * 8u;
-  // rounds a slot runs, spread over the 4 issue-priority levels (k_transport)
-  const uint32_t max_rounds = (host_pkt_blocks<WG_MODE_SEAL>(max_len) + 7u) / 8u;
-#ifndef WG_PRIO
-  P.prio_step = 0;
-#else
-  P.prio_step = std::max<uint32_t>(1u, (uint32_t)((per_slot * max_rounds + 3u) / 4u));
-#endif
+  uint32_t grid = 0;
   bool ordered = false;
-  if (!(flags & WG_F_UNIFORM) && per_slot > 1) {  // longest-first order (LPT) for the snake
-    int rc;
-    if ((rc = c->lpt_hist.ensure(sizeof(uint32_t) * 2 * wgt::LPT_BINS)) != WG_OK) return rc;
-    if ((rc = c->lpt_order.ensure(sizeof(uint32_t) * (size_t)n)) != WG_OK) return rc;
-    if ((rc = ws_acquire(c, s)) != WG_OK) return rc;
-    uint32_t* hist = (uint32_t*)c->lpt_hist.p;
-    uint32_t* cursor = hist + wgt::LPT_BINS;
-    HIPTRY(hipMemsetAsync(hist, 0, sizeof(uint32_t) * wgt::LPT_BINS, s));
-    const uint32_t hgrid = std::min<uint32_t>((n + 255u) / 256u, 1024u);
-    hipLaunchKernelGGL((wgt::k_lpt_hist<MODE>), dim3(hgrid), dim3(256), 0, s, desc, n, max_len, hist);
-    hipLaunchKernelGGL(wgt::k_lpt_offsets, dim3(1), dim3(256), 0, s, (const uint32_t*)hist, cursor);
-    hipLaunchKernelGGL((wgt::k_lpt_scatter<MODE>), dim3((n + 255u) / 256u), dim3(256), 0, s, desc, n, max_len, cursor,
-                       (uint32_t*)c->lpt_order.p);
-    HIPTRY(hipGetLastError());
-    P.order = (const uint32_t*)c->lpt_order.p;
-    ordered = true;
-  }
+  const uint64_t cap_slots = 8ull * std::max<uint32_t>(c->resident_waves[MODE == WG_MODE_OPEN], wgt::TW);
+  int rc = plan_transport<MODE>(c, desc, n, in, in_size, out, out_size, status, max_len, flags, s, cap_slots,
+                                c->lpt_hist, c->lpt_order, &P, &grid, &ordered);
+  if (rc != WG_OK) return rc;
   hipEvent_t ev;
   record_start(c, s, &ev);
   hipLaunchKernelGGL((wgt::k_transport<MODE>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
@@ -457,7 +478,7 @@ int wg_ctx_destroy(wg_ctx* c) {
     (void)hipEventDestroy(e.second);
   }
   for (DevBuf* b : {&c->plan_nb, &c->plan_prefix, &c->plan_tiles, &c->plan_ntiles, &c->plan_tmp, &c->lpt_hist,
-                    &c->lpt_order, &c->h_desc, &c->h_in, &c->h_out, &c->h_aad, &c->h_status, &c->h_keys})
+                    &c->lpt_order, &c->lpt_hist2, &c->lpt_order2, &c->h_desc, &c->h_in, &c->h_out, &c->h_aad, &c->h_status, &c->h_keys})
     b->release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -548,6 +569,61 @@ int wg_open_batch(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, 
   std::lock_guard<std::mutex> lk(c->mu);
   return launch_transport<WG_MODE_OPEN>(c, desc, n, in, in_size, out, out_size, status, max_len, flags,
                                        pick_stream(c, stream));
+}
+
+// Seal one batch and open another in one k_duplex launch (wg_duplex_batch).
+int wg_duplex_batch(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, void* stream) {
+  if (!c || !sb || !ob) return fail(WG_EINVAL, "NULL argument");
+  if (sb->flags & ~kFlagsKnown) return fail(WG_EINVAL, "unknown seal flag bits 0x%x", sb->flags & ~kFlagsKnown);
+  if (ob->flags & ~WG_F_UNIFORM) return fail(WG_EINVAL, "open takes only WG_F_UNIFORM (flags 0x%x)", ob->flags);
+  if (ob->n && !ob->status) return fail(WG_EINVAL, "open needs a status array");
+  DeviceGuard g(c->device);
+  hipStream_t s = pick_stream(c, stream);
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    if ((sb->flags & WG_F_FRAME) && !c->receivers)
+      return fail(WG_EINVAL, "WG_F_FRAME without a receiver table (wg_ctx_set_receivers)");
+    const bool fused = c->kern == KERN_TRANSPORT && sb->n && ob->n;
+    if (fused) {
+      for (const wg_batch* b : {sb, ob}) {
+        if (!b->desc || (((uintptr_t)b->desc) & 15u))
+          return fail(WG_EINVAL, "descriptor array must be non-NULL and 16-byte aligned");
+        if (!b->in || !b->out) return fail(WG_EINVAL, "NULL buffer");
+        if (b->max_len > WG_MAX_PACKET) return fail(WG_E2BIG, "max_len %u > WG_MAX_PACKET", b->max_len);
+      }
+      // the two halves share the machine: each plans with half of the resident slots
+      const uint64_t cap = 4ull * std::max<uint32_t>(std::min(c->resident_waves[0], c->resident_waves[1]), wgt::TW);
+      wgt::TransportParams PS{}, PO{};
+      uint32_t gs = 0, go = 0;
+      bool os = false, oo = false;
+      int rc = plan_transport<WG_MODE_SEAL>(c, sb->desc, sb->n, sb->in, sb->in_size, sb->out, sb->out_size, nullptr,
+                                            sb->max_len, sb->flags, s, cap, c->lpt_hist, c->lpt_order, &PS, &gs, &os);
+      if (rc != WG_OK) return rc;
+      rc = plan_transport<WG_MODE_OPEN>(c, ob->desc, ob->n, ob->in, ob->in_size, ob->out, ob->out_size, ob->status,
+                                        ob->max_len, ob->flags, s, cap, c->lpt_hist2, c->lpt_order2, &PO, &go, &oo);
+      if (rc != WG_OK) return rc;
+      hipEvent_t ev;
+      record_start(c, s, &ev);
+      hipLaunchKernelGGL(wgt::k_duplex, dim3(gs + go), dim3(64 * wgt::TW), 0, s, PS, PO, gs, go);
+      const hipError_t e = hipGetLastError();
+      record_end(c, s, ev);
+      if (e != hipSuccess) return fail(WG_EDEVICE, "k_duplex launch: %s", hipGetErrorString(e));
+      if ((os || oo) && (rc = ws_release(c, s)) != WG_OK) return rc;
+    } else {  // another kernel selected, or one side empty: the two launches in turn
+      int rc = launch_transport<WG_MODE_SEAL>(c, sb->desc, sb->n, sb->in, sb->in_size, sb->out, sb->out_size, nullptr,
+                                              sb->max_len, sb->flags, s);
+      if (rc != WG_OK) return rc;
+      rc = launch_transport<WG_MODE_OPEN>(c, ob->desc, ob->n, ob->in, ob->in_size, ob->out, ob->out_size, ob->status,
+                                          ob->max_len, ob->flags, s);
+      if (rc != WG_OK) return rc;
+    }
+    if (!(sb->flags & WG_F_FRAME) || sb->n == 0) return WG_OK;
+    hipLaunchKernelGGL(wgt::k_frame_seal, dim3((sb->n + 255u) / 256u), dim3(256), 0, s, sb->desc, sb->n, c->receivers,
+                       sb->max_len, c->key_slots, sb->in_size, sb->out, sb->out_size);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(WG_EDEVICE, "k_frame_seal launch: %s", hipGetErrorString(e));
+  }
+  return WG_OK;
 }
 
 int wg_frame_seal(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint32_t* receivers, uint8_t* out,

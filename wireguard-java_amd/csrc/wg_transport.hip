@@ -214,17 +214,15 @@ __device__ __forceinline__ uint32_t opaque_lane() {
   return x;
 }
 
+// The per-wave body of k_transport (and of each half of k_duplex): workgroup `blk` of the
+// direction's grid; img / rec are this wave's 4-KB image and slot records in LDS.
 template <int MODE>
-__global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8))) k_transport(TransportParams P) {
+__device__ __forceinline__ void transport_body(const TransportParams& P, uint32_t blk, uint32_t wv, uint4* const img,
+                                               SlotRec* const rec) {
   static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
   if (P.prio_step) __builtin_amdgcn_s_setprio(3);  // first instruction: a fresh wave is never starved
-  __shared__ uint4 img_[TW][4 * 64];     // 4 KB per wave: [chunk q][lane] = the round's payload / MAC input
-  __shared__ SlotRec rec_[TW][8];        // 1 KB per wave
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint4* const img = img_[wv];
-  SlotRec* const rec = rec_[wv];
   const uint32_t S = P.slots;
-  const uint32_t g = (blockIdx.x * TW + wv) * 8u + (opaque_lane() >> 3);
+  const uint32_t g = (blk * TW + wv) * 8u + (opaque_lane() >> 3);
 
   // descriptor prefetch: dword j of the next packet's wg_pkt (32 B = 8 dwords, one per lane)
   uint32_t gen = 0;
@@ -547,7 +545,49 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
     wave_lds_sync();  // this round's image and records before the next round rewrites them
     WG_PH(5);
   }
-  WG_PH_STORE(blockIdx.x * TW + wv);
+  WG_PH_STORE(blk * TW + wv);
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8))) k_transport(TransportParams P) {
+  __shared__ uint4 img_[TW][4 * 64];  // 4 KB per wave: [chunk q][lane] = the round's payload / MAC input
+  __shared__ SlotRec rec_[TW][8];     // 1 KB per wave
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  transport_body<MODE>(P, blockIdx.x, wv, img_[wv], rec_[wv]);
+}
+
+// One launch, two directions (wg_duplex_batch): a node's outgoing batch sealed and its
+// incoming batch opened side by side. Workgroups [0, 2m) alternate seal / open (m = the
+// smaller grid), the rest belong to the larger direction; each half runs exactly the
+// k_transport body on its own grid, so the bytes written are those of the two separate
+// launches. The two halves share the LDS declared here (one image + records per wave).
+__global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)))
+k_duplex(TransportParams S, TransportParams O, uint32_t seal_blocks, uint32_t open_blocks) {
+  __shared__ uint4 img_[TW][4 * 64];
+  __shared__ SlotRec rec_[TW][8];
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t m = min(seal_blocks, open_blocks);
+  const uint32_t b = blockIdx.x;
+  bool seal;
+  uint32_t idx;
+#ifdef WG_DUPLEX_SPLIT  // A/B build: all seal workgroups first
+  if (false) {
+#else
+  if (b < 2u * m) {
+#endif
+    seal = (b & 1u) == 0u;
+    idx = b >> 1;
+  } else {
+#ifdef WG_DUPLEX_SPLIT
+    seal = b < seal_blocks;
+    idx = seal ? b : b - seal_blocks;
+#else
+    seal = seal_blocks > open_blocks;
+    idx = b - m;
+#endif
+  }
+  if (seal) transport_body<WG_MODE_SEAL>(S, idx, wv, img_[wv], rec_[wv]);
+  else transport_body<WG_MODE_OPEN>(O, idx, wv, img_[wv], rec_[wv]);
 }
 
 // ---- longest-first order for mixed-length batches (LPT) ----------------------------------

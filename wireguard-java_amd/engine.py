@@ -135,6 +135,19 @@ class Engine:
                                         out.numel(), status.data_ptr(), max_len, L.WG_F_UNIFORM if uniform else 0,
                                         stream if stream is not None else _torch_stream()))
 
+    def duplex(self, seal_desc, seal_in, seal_out, seal_max_len: int, open_desc, open_in, open_out, status,
+               open_max_len: int, uniform: bool = False, frame: bool = False, stream: int | None = None):
+        """wg_duplex_batch: seal one batch and open another in one launch (the open batch must not
+        read what the seal batch writes). Same tensors as seal() / open()."""
+        u = L.WG_F_UNIFORM if uniform else 0
+        sb = L.WgBatch(seal_desc.data_ptr(), seal_in.data_ptr(), seal_out.data_ptr(), None, seal_in.numel(),
+                       seal_out.numel(), seal_desc.shape[0], seal_max_len, u | (L.WG_F_FRAME if frame else 0), 0)
+        ob = L.WgBatch(open_desc.data_ptr(), open_in.data_ptr(), open_out.data_ptr(),
+                       status.data_ptr() if status is not None else None, open_in.numel(), open_out.numel(),
+                       open_desc.shape[0], open_max_len, u, 0)
+        L.check(self._lib.wg_duplex_batch(self.ctx, ctypes.byref(sb), ctypes.byref(ob),
+                                          stream if stream is not None else _torch_stream()))
+
     # ---- receive side after open (wg_rx_check) -------------------------------------
     def filter_set(self, filter_id: int, prefixes) -> None:
         """wg_filter_set from (address string or ipaddress object, prefix_len) pairs, as
