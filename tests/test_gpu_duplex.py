@@ -24,7 +24,7 @@ def _batch(seed, n, lengths, nkeys, ctr_base=0, pre=0):
     """Packets at 16-B aligned strides; `pre` bytes of header room in front of each."""
     W = wg()
     S = ((lengths + 16 + 15) // 16) * 16 + pre
-    off = (np.concatenate([[0], np.cumsum(S)[:-1]]) + pre).astype(np.uint64)
+    off = (np.cumsum(S) - S + pre).astype(np.uint64)
     total = int(S.sum())
     desc = W.pack_desc(off, off, ctr_base + np.arange(n, dtype=np.uint64), lengths, np.arange(n) % nkeys)
     pt = splitmix_np(seed, total)
@@ -54,7 +54,7 @@ def _run(engine, n_seal, n_open, lens_seal, lens_open, nkeys, uniform, forge_eve
     st = torch.full((max(n_open, 1),), 7, dtype=torch.int32, device=dev)
     rx = None
     if frame:
-        rx = torch.arange(1000, 1000 + nkeys, dtype=torch.int32, device=dev)
+        rx = torch.arange(1000, 1000 + engine.key_slots, dtype=torch.int32, device=dev)
         engine.set_receivers(rx)
     maxs = int(lens_seal.max()) if n_seal else 0
     maxo = int(lens_open.max()) if n_open else 0
@@ -68,7 +68,8 @@ def _run(engine, n_seal, n_open, lens_seal, lens_open, nkeys, uniform, forge_eve
         O.seal_batch(sdesc, spt, ref[:stotal], keys, threads=16)
     got = dsct.cpu().numpy()
     if frame:
-        O.frame_headers(sdesc, np.arange(1000, 1000 + nkeys, dtype=np.uint32), ref, 4096, in_size=stotal,
+        O.frame_headers(sdesc, np.arange(1000, 1000 + engine.key_slots, dtype=np.uint32), ref, engine.key_slots,
+                        in_size=stotal,
                         max_len=maxs)
     assert np.array_equal(got, ref)
     # open half: statuses, plaintexts, forged packets zero-filled

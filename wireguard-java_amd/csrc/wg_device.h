@@ -92,6 +92,35 @@ __device__ __forceinline__ void chacha20_block_lds(const uint4* key_lds, uint32_
   out[8] = x8 + kb.x; out[9] = x9 + kb.y; out[10] = x10 + kb.z; out[11] = x11 + kb.w;
   out[12] = x12 + ctr; out[13] = x13 + n0; out[14] = x14 + n1; out[15] = x15 + n2;
 }
+// One ChaCha20 column quarter round on its own (the per-packet part of the first round).
+__device__ __forceinline__ void chacha20_qr(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) { WG_QR(a, b, c, d) }
+
+// Same block with the first column round of columns 1..3 already done: they depend only on
+// the key and the nonce (state words 13..15), not on the block counter, so a packet computes
+// them once (H = {x1, x5, x9, x13, x2, x6, x10, x14, x3, x7, x11, x15} after that round)
+// and every block of the packet starts from column 0's quarter round.
+__device__ __forceinline__ void chacha20_block_hoisted(const uint4* key_lds, uint32_t ctr, uint32_t n0, uint32_t n1,
+                                                       uint32_t n2, const uint32_t H[12], uint32_t out[16]) {
+  uint4 ka = key_lds[0], kb = key_lds[1];
+  uint32_t x0 = 0x61707865u, x4 = ka.x, x8 = kb.x, x12 = ctr;
+  uint32_t x1 = H[0], x5 = H[1], x9 = H[2], x13 = H[3];
+  uint32_t x2 = H[4], x6 = H[5], x10 = H[6], x14 = H[7];
+  uint32_t x3 = H[8], x7 = H[9], x11 = H[10], x15 = H[11];
+  WG_QR(x0, x4, x8, x12)
+  WG_QR(x0, x5, x10, x15) WG_QR(x1, x6, x11, x12) WG_QR(x2, x7, x8, x13) WG_QR(x3, x4, x9, x14)
+#pragma unroll 3
+  for (int r = 1; r < 10; ++r) {
+    WG_QR(x0, x4, x8, x12) WG_QR(x1, x5, x9, x13) WG_QR(x2, x6, x10, x14) WG_QR(x3, x7, x11, x15)
+    WG_QR(x0, x5, x10, x15) WG_QR(x1, x6, x11, x12) WG_QR(x2, x7, x8, x13) WG_QR(x3, x4, x9, x14)
+  }
+  asm volatile("" ::: "memory");
+  ka = key_lds[0];
+  kb = key_lds[1];
+  out[0] = x0 + 0x61707865u; out[1] = x1 + 0x3320646eu; out[2] = x2 + 0x79622d32u; out[3] = x3 + 0x6b206574u;
+  out[4] = x4 + ka.x; out[5] = x5 + ka.y; out[6] = x6 + ka.z; out[7] = x7 + ka.w;
+  out[8] = x8 + kb.x; out[9] = x9 + kb.y; out[10] = x10 + kb.z; out[11] = x11 + kb.w;
+  out[12] = x12 + ctr; out[13] = x13 + n0; out[14] = x14 + n1; out[15] = x15 + n2;
+}
 #undef WG_QR
 #undef WG_QR_SDWA
 
