@@ -52,7 +52,28 @@ def main():
             tot += a.elapsed_time(b)
         out[name + "_us"] = round(tot / reps * 1e3, 2)
         out[name + "_status_hist"] = np.bincount(st.cpu().numpy(), minlength=7).tolist()
+    # the replay window over 1024 key slots (64 packets per slot, slot = i mod 1024)
+    eng2 = W.Engine(0, key_slots=1024)
+    d2 = torch.from_numpy(W.desc_as_int64(W.pack_desc(np.arange(n) * S, np.arange(n) * S, np.arange(n) // 1024, L,
+                                                      np.arange(n) % 1024))).to(dev)
+    eng2.replay_enable(8192)
+    for _ in range(10):
+        st.copy_(st0)
+        eng2.rx_check(d2, dpt, st, 2)
+    torch.cuda.synchronize()
+    tot = 0.0
+    for _ in range(200):
+        st.copy_(st0)
+        eng2.replay_enable(8192)
+        a.record()
+        eng2.rx_check(d2, dpt, st, 2)
+        b.record()
+        torch.cuda.synchronize()
+        tot += a.elapsed_time(b)
+    out["replay_1024_slots_us"] = round(tot / 200 * 1e3, 2)
+    out["replay_1024_slots_status_hist"] = np.bincount(st.cpu().numpy(), minlength=7).tolist()
     print(json.dumps(out))
+    eng2.close()
     eng.close()
 
 

@@ -32,6 +32,11 @@
 // W behind an EARLIER packet of the same batch (but not behind the window at the batch's
 // start) is accepted, where a one-packet-at-a-time window would reject it. No counter is
 // ever accepted twice. oracle/rx.py restates these rules one packet at a time.
+// Kernels: k_rp_order flags a batch whose (slot, counter) pairs do not strictly increase with
+// the index (only then can a pair repeat); k_rp_insert claims one entry per (slot, counter) pair in an open-addressing table
+// (lowest index by atomicMin), k_rp_decide judges against the old window, k_rp_advance moves
+// each slot's window, k_rp_mark sets the ring bits and empties the table again. Atomics on a
+// shared address (a slot's new top, a window word) are aggregated per workgroup first.
 #pragma once
 
 namespace {
@@ -49,7 +54,13 @@ struct RxState {
   // replay window
   uint32_t window = 0;      // W bits (0: disabled)
   DevBuf d_top, d_bits;     // per slot: u64 top; W/64 u64 words
-  DevBuf d_newtop, d_hist, d_off, d_tab_key, d_tab_idx, d_scan_tmp;
+  DevBuf d_newtop;          // per slot: the window's new top while a batch is checked (== top between calls)
+  DevBuf d_tab;             // (slot, counter) -> lowest batch index, open addressing; all empty between calls
+  uint32_t tab_size = 0;    // entries (a power of two >= 2n)
+  DevBuf d_pos;             // per packet: its (slot, counter) entry in d_tab, or ~0
+  DevBuf d_flag;            // k_rp_order's flag (0 between calls)
+  hipEvent_t ev = nullptr;  // last use of the replay scratch, and its stream (stream-ordered reuse)
+  hipStream_t ev_stream = (hipStream_t)-1;
 };
 
 // ---- host: IPFilter.insert as a binary trie, then stride-8 tables -------------------------
@@ -102,9 +113,10 @@ int rx_get(wg_ctx* c, RxState** out) {
 void rx_free(wg_ctx* c) {
   if (!c->rx) return;
   RxState* r = c->rx;
-  for (DevBuf* b : {&r->d_entries, &r->d_hdr, &r->d_slot_filter, &r->d_top, &r->d_bits, &r->d_newtop, &r->d_hist,
-                    &r->d_off, &r->d_tab_key, &r->d_tab_idx, &r->d_scan_tmp})
+  for (DevBuf* b : {&r->d_entries, &r->d_hdr, &r->d_slot_filter, &r->d_top, &r->d_bits, &r->d_newtop, &r->d_tab,
+                    &r->d_pos, &r->d_flag})
     b->release();
+  if (r->ev) (void)hipEventDestroy(r->ev);
   delete r;
   c->rx = nullptr;
 }
@@ -114,6 +126,7 @@ int rx_reset_slots(wg_ctx* c, uint32_t first, uint32_t n, hipStream_t s) {
   RxState* r = c->rx;
   if (!r || !r->window || !n) return WG_OK;
   HIPTRY(hipMemsetAsync((uint64_t*)r->d_top.p + first, 0, (size_t)n * 8, s));
+  HIPTRY(hipMemsetAsync((uint64_t*)r->d_newtop.p + first, 0, (size_t)n * 8, s));
   const size_t words = r->window / 64;
   HIPTRY(hipMemsetAsync((uint64_t*)r->d_bits.p + (size_t)first * words, 0, (size_t)n * words * 8, s));
   return WG_OK;
@@ -141,10 +154,10 @@ struct RxParams {
   uint64_t* top;
   uint64_t* bits;
   uint64_t* newtop;
-  uint32_t* hist;
-  const uint32_t* off;
-  uint64_t* tab_key;
-  uint32_t* tab_idx;
+  uint32_t* tab;
+  uint32_t tab_size;
+  uint32_t* pos;
+  uint32_t* unsorted;  // 0 while the batch's (slot, counter) pairs strictly increase with the index
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -189,6 +202,10 @@ __device__ __forceinline__ void wave_group(bool active, uint64_t key, uint64_t v
     const uint64_t lk = shfl_u64(key, leader);
     const bool mine = active && key == lk;
     const uint64_t m = __ballot(mine);
+    if (__popcll(m) == 1) {  // keys mostly distinct in this wave: one atomic per lane (no contention)
+      if (active) f(key, 1u, val, val);
+      break;
+    }
     uint64_t mx = 0, orv = 0;
     if constexpr (MAX) {
       const uint32_t hi = wave_reduce<false>(mine ? (uint32_t)(val >> 32) : 0u);
@@ -205,9 +222,6 @@ __device__ __forceinline__ void wave_group(bool active, uint64_t key, uint64_t v
   }
 }
 
-// open-addressing slot of counter c in a table region of `size` entries (multiply-high)
-__device__ __forceinline__ uint64_t rp_hash(uint64_t c, uint64_t size) { return __umul64hi(mix64(c), size); }
-
 __device__ __forceinline__ bool rp_candidate(const RxParams& P, uint32_t i, uint32_t& slot, uint64_t& ctr) {
   if (P.status[i] != WG_PKT_OK) return false;
   const wg_pkt d = P.desc[i];
@@ -217,40 +231,88 @@ __device__ __forceinline__ bool rp_candidate(const RxParams& P, uint32_t i, uint
   return true;
 }
 
-// also initialises this batch's scratch: the counter table (2n entries) and newtop = top
-__global__ void __launch_bounds__(256) k_rp_count(RxParams P) {
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  if (i < P.n) {
-    P.tab_key[2ull * i] = kEmptyKey;
-    P.tab_key[2ull * i + 1] = kEmptyKey;
-    P.tab_idx[2ull * i] = ~0u;
-    P.tab_idx[2ull * i + 1] = ~0u;
+// A whole workgroup's atomics per distinct key: every wave groups its lanes by key
+// (wave_group), the groups' leaders list (key, max, or) in LDS, and one lane per distinct key
+// of the workgroup issues the atomic (a single-slot batch: one atomic per workgroup instead of
+// one per wave; same-address atomics serialise). Every thread of the block must call it.
+constexpr uint32_t kGroupCap = 64;
+template <bool MAX, bool OR, class F>
+__device__ __forceinline__ void block_group(bool active, uint64_t key, uint64_t val, F f) {
+  __shared__ uint64_t g_key[kGroupCap], g_max[kGroupCap], g_or[kGroupCap];
+  __shared__ uint32_t g_n;
+  if (threadIdx.x == 0) g_n = 0;
+  __syncthreads();
+  wave_group<MAX, OR>(active, key, val, [&](uint64_t k, uint32_t, uint64_t mx, uint64_t orv) {
+    const uint32_t e = atomicAdd(&g_n, 1u);
+    if (e < kGroupCap) {
+      g_key[e] = k;
+      g_max[e] = mx;
+      g_or[e] = orv;
+    } else {
+      f(k, mx, orv);  // more distinct keys than the list holds: this group's atomic directly
+    }
+  });
+  __syncthreads();
+  const uint32_t cnt = min(g_n, kGroupCap);
+  if (threadIdx.x < cnt) {
+    const uint64_t k = g_key[threadIdx.x];
+    bool first = true;
+    for (uint32_t e = 0; e < threadIdx.x; ++e) first = first && g_key[e] != k;
+    if (first) {
+      uint64_t mx = 0, orv = 0;
+      for (uint32_t e = threadIdx.x; e < cnt; ++e)
+        if (g_key[e] == k) {
+          mx = g_max[e] > mx ? g_max[e] : mx;
+          orv |= g_or[e];
+        }
+      f(k, mx, orv);
+    }
   }
-  if (i < P.key_slots) P.newtop[i] = P.top[i];
-  uint32_t slot = 0;
-  uint64_t c = 0;
-  const bool act = i < P.n && rp_candidate(P, i, slot, c);
-  wave_group<false, false>(act, slot, 0ull, [&](uint64_t k, uint32_t cnt, uint64_t, uint64_t) { atomicAdd(&P.hist[k], cnt); });
 }
 
-// each slot's packets share a region of 2 x count open-addressing entries keyed by counter;
-// the entry keeps the lowest batch index that carried the counter
+// entry of (slot, counter) in the table of `size` (a power of two) entries (multiply-high)
+__device__ __forceinline__ uint32_t rp_hash(uint32_t slot, uint64_t c, uint32_t size) {
+  return (uint32_t)__umul64hi(mix64(c ^ ((uint64_t)slot * 0x9E3779B97F4A7C15ull)), (uint64_t)size);
+}
+
+// A batch whose (key slot, counter) pairs strictly increase with the batch index (one peer's
+// in-order stream, or streams sorted by slot) holds no pair twice: the table is skipped. Only
+// a wave that finds an out-of-order neighbour raises the flag (no atomics in the common case).
+__global__ void __launch_bounds__(256) k_rp_order(RxParams P) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  bool bad = false;
+  if (i > 0 && i < P.n) {
+    const wg_pkt a = P.desc[i - 1], b = P.desc[i];
+    bad = !(a.key_slot < b.key_slot || (a.key_slot == b.key_slot && a.counter < b.counter));
+  }
+  if (__any(bad) && (threadIdx.x & 63u) == 0) atomicOr(P.unsorted, 1u);
+}
+
+// every candidate claims the entry of its (slot, counter): the first claim stores its batch index,
+// later claims of the same pair lower it to the smallest index (atomicMin); pos[i] = the entry
 __global__ void __launch_bounds__(256) k_rp_insert(RxParams P) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  uint32_t slot;
+  if (i >= P.n) return;
+  uint32_t slot, pos = ~0u;
   uint64_t c;
-  if (i >= P.n || !rp_candidate(P, i, slot, c) || c >= kRejectAfter) return;
-  const uint64_t base = 2ull * P.off[slot], size = 2ull * P.hist[slot];
-  uint64_t h = rp_hash(c, size);
-  for (uint64_t probe = 0; probe < size; ++probe) {
-    const unsigned long long old =
-        atomicCAS((unsigned long long*)&P.tab_key[base + h], (unsigned long long)kEmptyKey, (unsigned long long)c);
-    if (old == kEmptyKey || old == c) {
-      atomicMin(&P.tab_idx[base + h], i);
-      return;
+  if (*P.unsorted && rp_candidate(P, i, slot, c) && c < kRejectAfter) {
+    const uint32_t mask = P.tab_size - 1u;
+    uint32_t h = rp_hash(slot, c, P.tab_size);
+    for (uint32_t probe = 0; probe < P.tab_size; ++probe, h = (h + 1u) & mask) {
+      const uint32_t old = atomicCAS(&P.tab[h], ~0u, i);
+      if (old == ~0u) {
+        pos = h;
+        break;
+      }
+      const wg_pkt o = P.desc[old];  // an index of the same pair, or of another pair on this entry
+      if (o.key_slot == slot && o.counter == c) {
+        atomicMin(&P.tab[h], i);
+        pos = h;
+        break;
+      }
     }
-    h = h + 1 == size ? 0 : h + 1;
   }
+  P.pos[i] = pos;
 }
 
 __device__ __forceinline__ bool bit_test(const uint64_t* bits, uint32_t W, uint32_t slot, uint64_t c) {
@@ -258,26 +320,20 @@ __device__ __forceinline__ bool bit_test(const uint64_t* bits, uint32_t W, uint3
   return (bits[(uint64_t)slot * (W / 64) + pos / 64] >> (pos % 64)) & 1ull;
 }
 
+// a candidate passes if it is the lowest index of its (slot, counter) and the window as it stood
+// before the batch takes it; newtop[slot] = max(top, passing counter + 1)
 __global__ void __launch_bounds__(256) k_rp_decide(RxParams P) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   uint32_t slot = 0;
   uint64_t c = 0;
   const bool cand = i < P.n && rp_candidate(P, i, slot, c);
   bool ok = cand && c < kRejectAfter;
-  if (ok) {  // first of its (slot, counter) in the batch? (cand lanes only)
-    const uint64_t base = 2ull * P.off[slot], size = 2ull * P.hist[slot];
-    uint64_t h = rp_hash(c, size);
-    for (uint64_t probe = 0; probe < size; ++probe) {
-      if (P.tab_key[base + h] == c) break;
-      h = h + 1 == size ? 0 : h + 1;
-    }
-    ok = P.tab_idx[base + h] == i;
-  }
+  if (ok && *P.unsorted) ok = P.tab[P.pos[i]] == i;
   if (ok) {
     const uint64_t top = P.top[slot];
     if (c < top) ok = top - c <= P.window && !bit_test(P.bits, P.window, slot, c);
   }
-  wave_group<true, false>(ok, slot, c + 1, [&](uint64_t k, uint32_t, uint64_t mx, uint64_t) {
+  block_group<true, false>(ok, slot, c + 1, [&](uint64_t k, uint64_t mx, uint64_t) {
     atomicMax((unsigned long long*)&P.newtop[k], (unsigned long long)mx);
   });
   if (cand && !ok) P.status[i] = WG_PKT_REPLAY;
@@ -309,6 +365,8 @@ __global__ void __launch_bounds__(256) k_rp_advance(RxParams P) {
   P.top[slot] = nt;
 }
 
+// accepted counters still inside the advanced window get their ring bit; the table entries this
+// batch used are emptied again (nothing reads the table in this kernel)
 __global__ void __launch_bounds__(256) k_rp_mark(RxParams P) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   uint32_t slot = 0;
@@ -317,9 +375,11 @@ __global__ void __launch_bounds__(256) k_rp_mark(RxParams P) {
   if (act) act = P.top[slot] - c <= P.window;          // top advanced; c < top here
   const uint64_t pos = act ? c % P.window : 0ull;
   const uint64_t word = (uint64_t)slot * (P.window / 64) + pos / 64;
-  wave_group<false, true>(act, word, 1ull << (pos % 64), [&](uint64_t k, uint32_t, uint64_t, uint64_t orv) {
+  block_group<false, true>(act, word, 1ull << (pos % 64), [&](uint64_t k, uint64_t, uint64_t orv) {
     atomicOr((unsigned long long*)&P.bits[k], (unsigned long long)orv);
   });
+  if (i < P.n && P.pos[i] != ~0u) P.tab[P.pos[i]] = ~0u;
+  if (i == 0) *P.unsorted = 0u;  // k_rp_decide was its last reader: 0 again for the next batch
 }
 
 // keepalive / IP version / AllowedIPs, one thread per packet
@@ -455,9 +515,7 @@ int wg_replay_enable(wg_ctx* c, uint32_t window_bits) {
   int rc;
   if ((rc = r->d_top.ensure((size_t)c->key_slots * 8)) != WG_OK ||
       (rc = r->d_newtop.ensure((size_t)c->key_slots * 8)) != WG_OK ||
-      (rc = r->d_bits.ensure((size_t)c->key_slots * (window_bits / 8))) != WG_OK ||
-      (rc = r->d_hist.ensure(((size_t)c->key_slots + 1) * 4)) != WG_OK ||
-      (rc = r->d_off.ensure(((size_t)c->key_slots + 1) * 4)) != WG_OK)
+      (rc = r->d_bits.ensure((size_t)c->key_slots * (window_bits / 8))) != WG_OK)
     return rc;
   if ((rc = rx_reset_slots(c, 0, c->key_slots, c->stream)) != WG_OK) return rc;
   HIPTRY(hipStreamSynchronize(c->stream));
@@ -515,31 +573,40 @@ int wg_rx_check(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* pt, ui
   const uint32_t grid = (n + 255u) / 256u;
   if (flags & WG_RX_REPLAY) {
     int rc;
-    if ((rc = r->d_tab_key.ensure((size_t)2 * n * 8)) != WG_OK || (rc = r->d_tab_idx.ensure((size_t)2 * n * 4)) != WG_OK)
-      return rc;
-    size_t tmp = 0;
-    HIPTRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, (uint32_t*)r->d_hist.p, (uint32_t*)r->d_off.p,
-                                            (int)c->key_slots + 1, s));
-    if ((rc = r->d_scan_tmp.ensure(tmp)) != WG_OK) return rc;
+    // the scratch (table, positions) is shared by the context's replay checks: a check on
+    // another stream first waits for the previous one
+    if (!r->ev) HIPTRY(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming));
+    if (r->ev_stream != s && r->ev_stream != (hipStream_t)-1) HIPTRY(hipStreamWaitEvent(s, r->ev, 0));
+    uint32_t T = 1024;
+    while (T < 2ull * n) T <<= 1;
+    if (T > r->tab_size || (size_t)n * 4 > r->d_pos.cap)
+      HIPTRY(hipDeviceSynchronize());  // the scratch is reallocated under earlier checks
+    if (T > r->tab_size) {  // (re)allocated: all entries empty (0xFF..)
+      if ((rc = r->d_tab.ensure((size_t)T * 4)) != WG_OK) return rc;
+      HIPTRY(hipMemsetAsync(r->d_tab.p, 0xFF, (size_t)T * 4, s));
+      r->tab_size = T;
+    }
+    if ((rc = r->d_pos.ensure((size_t)n * 4)) != WG_OK) return rc;
+    if (!r->d_flag.p) {
+      if ((rc = r->d_flag.ensure(4)) != WG_OK) return rc;
+      HIPTRY(hipMemsetAsync(r->d_flag.p, 0, 4, s));
+    }
     P.window = r->window;
     P.top = (uint64_t*)r->d_top.p;
     P.bits = (uint64_t*)r->d_bits.p;
     P.newtop = (uint64_t*)r->d_newtop.p;
-    P.hist = (uint32_t*)r->d_hist.p;
-    P.off = (const uint32_t*)r->d_off.p;
-    P.tab_key = (uint64_t*)r->d_tab_key.p;
-    P.tab_idx = (uint32_t*)r->d_tab_idx.p;
-    HIPTRY(hipMemsetAsync(r->d_hist.p, 0, ((size_t)c->key_slots + 1) * 4, s));
-    const uint32_t grid_c = (std::max(n, c->key_slots) + 255u) / 256u;
-    hipLaunchKernelGGL(wgrx::k_rp_count, dim3(grid_c), dim3(256), 0, s, P);
-    HIPTRY(hipGetLastError());
-    HIPTRY(hipcub::DeviceScan::ExclusiveSum(r->d_scan_tmp.p, tmp, (uint32_t*)r->d_hist.p, (uint32_t*)r->d_off.p,
-                                            (int)c->key_slots + 1, s));
+    P.tab = (uint32_t*)r->d_tab.p;
+    P.tab_size = r->tab_size;
+    P.pos = (uint32_t*)r->d_pos.p;
+    P.unsorted = (uint32_t*)r->d_flag.p;
+    hipLaunchKernelGGL(wgrx::k_rp_order, dim3(grid), dim3(256), 0, s, P);
     hipLaunchKernelGGL(wgrx::k_rp_insert, dim3(grid), dim3(256), 0, s, P);
     hipLaunchKernelGGL(wgrx::k_rp_decide, dim3(grid), dim3(256), 0, s, P);
     hipLaunchKernelGGL(wgrx::k_rp_advance, dim3((c->key_slots + 255u) / 256u), dim3(256), 0, s, P);
     hipLaunchKernelGGL(wgrx::k_rp_mark, dim3(grid), dim3(256), 0, s, P);
     HIPTRY(hipGetLastError());
+    HIPTRY(hipEventRecord(r->ev, s));
+    r->ev_stream = s;
   }
   if (flags & WG_RX_FILTER) {
     P.slot_filter = r->slot_filter_init ? (const uint32_t*)r->d_slot_filter.p : nullptr;
