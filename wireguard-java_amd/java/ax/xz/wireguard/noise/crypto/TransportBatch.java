@@ -143,6 +143,47 @@ public final class TransportBatch {
 	}
 
 	/**
+	 * Seals one device-resident batch and opens another in one kernel launch (wg_duplex_batch):
+	 * the node's outgoing packets (TransportManager.java:41) and its incoming ones (:79). The open
+	 * batch must not read bytes the seal batch writes in the same call.
+	 */
+	public static void duplexDevice(MemorySegment sealTable, int nSeal, MemorySegment sealIn, long sealInSize,
+	                                MemorySegment sealOut, long sealOutSize, int sealMaxLen,
+	                                MemorySegment openTable, int nOpen, MemorySegment openIn, long openInSize,
+	                                MemorySegment openOut, long openOutSize, MemorySegment status, int openMaxLen,
+	                                boolean uniform, MemorySegment stream) {
+		try (var arena = Arena.ofConfined()) {
+			var s = batch(arena, sealTable, nSeal, sealIn, sealInSize, sealOut, sealOutSize, MemorySegment.NULL,
+				sealMaxLen, uniform);
+			var o = batch(arena, openTable, nOpen, openIn, openInSize, openOut, openOutSize, status, openMaxLen,
+				uniform);
+			WgAead.check((int) WgAead.DUPLEX_BATCH.invokeExact(WgAead.CTX, s, o, stream));
+		} catch (RuntimeException e) {
+			throw e;
+		} catch (Throwable e) {
+			throw new RuntimeException(e);
+		}
+	}
+
+	// struct wg_batch {desc, in, out, status, in_size, out_size, n, max_len, flags, _reserved} (64 B)
+	private static MemorySegment batch(Arena arena, MemorySegment table, int n, MemorySegment in, long inSize,
+	                                   MemorySegment out, long outSize, MemorySegment status, int maxLen,
+	                                   boolean uniform) {
+		var b = arena.allocate(WgAead.BATCH_SIZE, 8);
+		b.set(ADDRESS, 0, table);
+		b.set(ADDRESS, 8, in);
+		b.set(ADDRESS, 16, out);
+		b.set(ADDRESS, 24, status);
+		b.set(JAVA_LONG, 32, inSize);
+		b.set(JAVA_LONG, 40, outSize);
+		b.set(JAVA_INT, 48, n);
+		b.set(JAVA_INT, 52, maxLen);
+		b.set(JAVA_INT, 56, uniform ? WgAead.WG_F_UNIFORM : 0);
+		b.set(JAVA_INT, 60, 0);
+		return b;
+	}
+
+	/**
 	 * A pinned, device-mapped host ring (wg_host_alloc): packet buffers allocated here make
 	 * {@link #sealHost} / {@link #openHost} zero-copy. Free with {@link #freeHostRing}.
 	 */

@@ -30,11 +30,11 @@ public final class WgAead {
 	/** wg_rx_check outcomes (TransportManager.processDecryptedTransport, TransportManager.java:98-119). */
 	public static final int WG_PKT_KEEPALIVE = 3, WG_PKT_BADIP = 4, WG_PKT_FILTERED = 5, WG_PKT_REPLAY = 6;
 	public static final int WG_RX_FILTER = 1, WG_RX_REPLAY = 2, WG_NO_FILTER = -1;
-	public static final long AEAD_DESC_SIZE = 64, PKT_DESC_SIZE = 32;
+	public static final long AEAD_DESC_SIZE = 64, PKT_DESC_SIZE = 32, BATCH_SIZE = 64;
 
 	static final MethodHandle SELFTEST, CTX_CREATE, LAST_ERROR, KEYS_SET, KEYS_ZERO, SEAL1, OPEN1, AEAD_HOST,
 		SEAL_BATCH, OPEN_BATCH, SYNC, SEAL_HOST, OPEN_HOST, HOST_ALLOC, HOST_FREE, FRAME_SEAL, PARSE_OPEN,
-		FILTER_SET, SLOT_FILTERS_SET, REPLAY_ENABLE, REPLAY_RESET, RX_CHECK;
+		FILTER_SET, SLOT_FILTERS_SET, REPLAY_ENABLE, REPLAY_RESET, RX_CHECK, DUPLEX_BATCH;
 
 	/** The process-wide context (one HIP device, its stream and its device key table). */
 	static final MemorySegment CTX;
@@ -82,6 +82,9 @@ public final class WgAead {
 			JAVA_INT));
 		RX_CHECK = down(linker, symbols, "wg_rx_check", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT,
 			ADDRESS, JAVA_LONG, ADDRESS, JAVA_INT, ADDRESS));
+		// outgoing seal + incoming open in one launch (two wg_batch structs of 64 bytes)
+		DUPLEX_BATCH = down(linker, symbols, "wg_duplex_batch", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS,
+			ADDRESS));
 
 		int device = Integer.getInteger("wg.device", 0);
 		KEY_SLOTS = Integer.getInteger("wg.keySlots", 65536);
