@@ -111,6 +111,25 @@ __device__ __forceinline__ uint32_t xor8(uint32_t v) {  // lane reads lane ^ X (
   return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1f | (X << 10));
 }
 
+// The same exchanges through DPP (VALU, no LDS round trip) for the dependent chains of the
+// r-power scan and the slot sum: row_shr:K (lane j reads j - K; lanes j < K of a slot get
+// garbage and must not use it), lane ^ 1, lane ^ 2 (quad_perm) and lane ^ 4 (two half moves).
+template <int K>
+__device__ __forceinline__ uint32_t shr8_dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 | K, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t xor1_dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+}
+__device__ __forceinline__ uint32_t xor2_dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+}
+__device__ __forceinline__ uint32_t xor4_dpp(uint32_t v) {
+  // lanes 4-7 of a slot (banks 1, 3) read j - 4 (row_shr:4), lanes 0-3 (banks 0, 2) read j + 4 (row_shl:4)
+  const int t = __builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xa, false);
+  return (uint32_t)__builtin_amdgcn_update_dpp(t, (int)v, 0x104, 0xf, 0x5, false);
+}
+
 // ---- validity of one transport descriptor (shared by seal, open and the framing) ----
 template <int MODE>
 __device__ __forceinline__ bool transport_valid(uint64_t in_off, uint64_t out_off, uint32_t len, uint32_t ks,
@@ -450,7 +469,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
 #endif
           uint32_t z[5], zs[5];
 #pragma unroll
-          for (int i = 0; i < 5; ++i) z[i] = __shfl(y[i], (int)(j >= st ? lane - st : lane), 64);
+          for (int i = 0; i < 5; ++i) z[i] = st == 1 ? shr8_dpp<1>(y[i]) : st == 2 ? shr8_dpp<2>(y[i]) : shr8_dpp<4>(y[i]);
           poly_scale5(z, zs);
           if (j >= st) poly_mul(y, z, zs);
         }
@@ -534,9 +553,9 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         }
 #pragma unroll
         for (int i = 0; i < 5; ++i) {  // slot sum (every lane of the slot ends with it)
-          acc[i] += xor8<1>(acc[i]);
-          acc[i] += xor8<2>(acc[i]);
-          acc[i] += xor8<4>(acc[i]);
+          acc[i] += xor1_dpp(acc[i]);
+          acc[i] += xor2_dpp(acc[i]);
+          acc[i] += xor4_dpp(acc[i]);
         }
         const uint4 ad = rec[s].addr;
         const uint8_t* inp = P.in + ((uint64_t)ad.x | ((uint64_t)ad.y << 32));
