@@ -322,17 +322,14 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
 #endif
   if (!(flags & WG_F_UNIFORM) && per_slot > 1) {  // longest-first order (LPT) for the snake
     int rc;
-    if ((rc = lpt_hist.ensure(sizeof(uint32_t) * 2 * wgt::LPT_BINS)) != WG_OK) return rc;
+    const uint32_t lgrid = std::max<uint32_t>(1u, std::min<uint32_t>(wgt::LPT_MAX_BLOCKS, (n + 1023u) / 1024u));
+    if ((rc = lpt_hist.ensure(sizeof(uint32_t) * wgt::LPT_MAX_BLOCKS * wgt::LPT_BINS)) != WG_OK) return rc;
     if ((rc = lpt_order.ensure(sizeof(uint32_t) * (size_t)n)) != WG_OK) return rc;
     if ((rc = ws_acquire(c, s)) != WG_OK) return rc;
-    uint32_t* hist = (uint32_t*)lpt_hist.p;
-    uint32_t* cursor = hist + wgt::LPT_BINS;
-    HIPTRY(hipMemsetAsync(hist, 0, sizeof(uint32_t) * wgt::LPT_BINS, s));
-    const uint32_t hgrid = std::min<uint32_t>((n + 255u) / 256u, 1024u);
-    hipLaunchKernelGGL((wgt::k_lpt_hist<MODE>), dim3(hgrid), dim3(256), 0, s, desc, n, max_len, hist);
-    hipLaunchKernelGGL(wgt::k_lpt_offsets, dim3(1), dim3(256), 0, s, (const uint32_t*)hist, cursor);
-    hipLaunchKernelGGL((wgt::k_lpt_scatter<MODE>), dim3((n + 255u) / 256u), dim3(256), 0, s, desc, n, max_len, cursor,
-                       (uint32_t*)lpt_order.p);
+    uint32_t* bh = (uint32_t*)lpt_hist.p;
+    hipLaunchKernelGGL((wgt::k_lpt_hist<MODE>), dim3(lgrid), dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len, bh);
+    hipLaunchKernelGGL((wgt::k_lpt_scatter<MODE>), dim3(lgrid), dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len,
+                       (const uint32_t*)bh, (uint32_t*)lpt_order.p);
     HIPTRY(hipGetLastError());
     P.order = (const uint32_t*)lpt_order.p;
     ordered = true;

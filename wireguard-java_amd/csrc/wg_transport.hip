@@ -645,50 +645,64 @@ __device__ __forceinline__ uint32_t lpt_key(const wg_pkt* d, uint32_t i, uint32_
   return (nb + 7u) >> 3;
 }
 
-template <int MODE>
-__global__ void __launch_bounds__(256) k_lpt_hist(const wg_pkt* d, uint32_t n, uint32_t max_len, uint32_t* hist) {
-  __shared__ uint32_t h[LPT_BINS];
-  for (uint32_t k = threadIdx.x; k < LPT_BINS; k += 256u) h[k] = 0;
-  __syncthreads();
-  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u)
-    atomicAdd(&h[lpt_key<MODE>(d, i, max_len)], 1u);
-  __syncthreads();
-  for (uint32_t k = threadIdx.x; k < LPT_BINS; k += 256u)
-    if (h[k]) atomicAdd(&hist[k], h[k]);
+// Two launches, no global atomics and no memset: k_lpt_hist writes one histogram per block
+// over a contiguous range of the batch; k_lpt_scatter (same grid) gives each block its base
+// per key from all blocks' histograms (keys above it in every block, this key in the blocks
+// before it) and ranks its packets in LDS.
+constexpr uint32_t LPT_THREADS = 1024, LPT_MAX_BLOCKS = 64;
+
+__device__ __forceinline__ void lpt_range(uint32_t n, uint32_t& lo, uint32_t& hi) {
+  const uint32_t per = (n + gridDim.x - 1) / gridDim.x;
+  lo = min(n, blockIdx.x * per);
+  hi = min(n, lo + per);
 }
 
-// cursor[k] = number of packets with a larger key (one workgroup)
-__global__ void __launch_bounds__(256) k_lpt_offsets(const uint32_t* hist, uint32_t* cursor) {
+template <int MODE>
+__global__ void __launch_bounds__(LPT_THREADS) k_lpt_hist(const wg_pkt* d, uint32_t n, uint32_t max_len,
+                                                          uint32_t* bh) {
   __shared__ uint32_t h[LPT_BINS];
-  for (uint32_t k = threadIdx.x; k < LPT_BINS; k += 256u) h[k] = hist[k];
+  for (uint32_t k = threadIdx.x; k < LPT_BINS; k += LPT_THREADS) h[k] = 0;
   __syncthreads();
-  if (threadIdx.x == 0) {
+  uint32_t lo, hi;
+  lpt_range(n, lo, hi);
+  for (uint32_t i = lo + threadIdx.x; i < hi; i += LPT_THREADS) atomicAdd(&h[lpt_key<MODE>(d, i, max_len)], 1u);
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < LPT_BINS; k += LPT_THREADS) bh[blockIdx.x * LPT_BINS + k] = h[k];
+}
+
+// order[pos] = packet, keys descending
+template <int MODE>
+__global__ void __launch_bounds__(LPT_THREADS) k_lpt_scatter(const wg_pkt* d, uint32_t n, uint32_t max_len,
+                                                             const uint32_t* bh, uint32_t* order) {
+  __shared__ uint32_t all[LPT_MAX_BLOCKS * LPT_BINS];  // every block's histogram (coalesced load)
+  __shared__ uint32_t tot[LPT_BINS], base[LPT_BINS];
+  for (uint32_t e = threadIdx.x; e < gridDim.x * LPT_BINS; e += LPT_THREADS) all[e] = bh[e];
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < LPT_BINS; k += LPT_THREADS) {
+    uint32_t t = 0, before = 0;
+    for (uint32_t b = 0; b < gridDim.x; ++b) {
+      const uint32_t v = all[b * LPT_BINS + k];
+      t += v;
+      before += b < blockIdx.x ? v : 0u;
+    }
+    tot[k] = t;
+    base[k] = before;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // packets with a larger key come first
     uint32_t acc = 0;
     for (int k = (int)LPT_BINS - 1; k >= 0; --k) {
-      const uint32_t c = h[k];
-      h[k] = acc;
+      const uint32_t c = tot[k];
+      tot[k] = acc;
       acc += c;
     }
   }
   __syncthreads();
-  for (uint32_t k = threadIdx.x; k < LPT_BINS; k += 256u) cursor[k] = h[k];
-}
-
-// order[pos] = packet: each workgroup reserves a range per key, then ranks its packets in it
-template <int MODE>
-__global__ void __launch_bounds__(256) k_lpt_scatter(const wg_pkt* d, uint32_t n, uint32_t max_len, uint32_t* cursor,
-                                                     uint32_t* order) {
-  __shared__ uint32_t cnt[LPT_BINS], base[LPT_BINS];
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  for (uint32_t k = threadIdx.x; k < LPT_BINS; k += 256u) cnt[k] = 0;
+  for (uint32_t k = threadIdx.x; k < LPT_BINS; k += LPT_THREADS) base[k] += tot[k];
   __syncthreads();
-  const uint32_t key = i < n ? lpt_key<MODE>(d, i, max_len) : 0u;
-  const uint32_t rank = i < n ? atomicAdd(&cnt[key], 1u) : 0u;
-  __syncthreads();
-  for (uint32_t k = threadIdx.x; k < LPT_BINS; k += 256u)
-    if (cnt[k]) base[k] = atomicAdd(&cursor[k], cnt[k]);
-  __syncthreads();
-  if (i < n) order[base[key] + rank] = i;
+  uint32_t lo, hi;
+  lpt_range(n, lo, hi);
+  for (uint32_t i = lo + threadIdx.x; i < hi; i += LPT_THREADS) order[atomicAdd(&base[lpt_key<MODE>(d, i, max_len)], 1u)] = i;
 }
 
 // ---- wire framing (TransportPacket.java:18-35) --------------------------------------------
