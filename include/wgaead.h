@@ -260,7 +260,9 @@ int wg_parse_open(wg_ctx* ctx, const uint8_t* wire_dev, uint64_t wire_size, cons
  * window_bits behind the highest counter accepted before this batch, or was already
  * accepted; the window then advances past this batch's accepted counters (the window slides
  * between batches). Asynchronous on `stream`; run it after wg_open_batch on
- * the same stream. pt / pt_size: the open's output buffer (plaintexts at out_off).
+ * the same stream. pt / pt_size: the open's output buffer (plaintexts at out_off). With
+ * WG_RX_REPLAY a batch holds at most 2^30 packets; checks on different streams of one context
+ * are ordered by the library (they share the window's scratch).
  *
  * wg_filter_set: AllowedIPs filter `filter_id` (< WG_MAX_FILTERS) from n prefixes, exactly as
  *   IPFilter.insert builds its trie (util/IPFilter.java:30-42), including its search rule:

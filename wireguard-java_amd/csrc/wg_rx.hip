@@ -577,6 +577,7 @@ int wg_rx_check(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* pt, ui
     // another stream first waits for the previous one
     if (!r->ev) HIPTRY(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming));
     if (r->ev_stream != s && r->ev_stream != (hipStream_t)-1) HIPTRY(hipStreamWaitEvent(s, r->ev, 0));
+    if (n > (1u << 30)) return fail(WG_EINVAL, "replay check of %u packets: at most 2^30 per batch", n);
     uint32_t T = 1024;
     while (T < 2ull * n) T <<= 1;
     if (T > r->tab_size || (size_t)n * 4 > r->d_pos.cap)
