@@ -20,7 +20,9 @@
 // broadcast (chacha20_block_hoisted: -3% VALU instructions on C1). Poly1305: the length block
 // is written into the image by the lane whose counter block holds it, so the Horner steps
 // read it like ciphertext; each step's product runs as five independent v_mad_u64_u32
-// chains (poly_mul_ilp: +1% instructions, no slower on C1, +3% on C2's mixed lengths).
+// chains (poly_mul_ilp: +1% instructions, no slower on C1, +3% on C2's mixed lengths). The
+// r-power scan and the slot sum exchange limbs through DPP (row_shr / quad_perm), which stays
+// in the VALU instead of an LDS round trip in the middle of a dependent chain.
 // Slots are persistent: slot g of S processes batch positions g, 2S-1-g, 2S+g, ... (a
 // snake over the grid). Mixed-length batches are first ordered longest-first on the
 // device (k_lpt_*), so the snake deals every slot one long and one short packet
