@@ -340,15 +340,16 @@ KERNELS = [("transport", 0, 0), ("wave1", 0, 0), ("tile", 0, 0)]
 @pytest.mark.parametrize("kern,lanes,variant", KERNELS)
 def test_every_transport_kernel_bit_exact(torch_dev, kern, lanes, variant):
     """each selectable transport kernel (k_transport, the round-1 k_wave kept
-    as the A/B baseline, k_tile) seals and opens bit-exact vs the oracle on a uniform
-    1420-B batch and on a mixed 0..3000-B batch, and rejects a tampered tag (status
-    BADTAG, plaintext scrubbed)."""
+    as the A/B baseline, k_tile) seals and opens
+    bit-exact vs the oracle on a uniform 1420-B batch and on a mixed 0..3000-B batch (with
+    and without WG_F_UNIFORM), and rejects a tampered tag (status BADTAG, plaintext
+    scrubbed)."""
     W = wg()
     eng = W.Engine(0, key_slots=64)
     try:
         eng.set_kernel(kern, lanes, variant)
-        for case, (lengths, uniform) in enumerate([([1420] * 777, True),
-                                                   (list(splitmix_np(11, 4 * 777).view("<u4") % 3001), False)]):
+        mixed = list(splitmix_np(11, 4 * 777).view("<u4") % 3001)
+        for case, (lengths, uniform) in enumerate([([1420] * 777, True), (mixed, False), (mixed, True)]):
             n = len(lengths)
             desc, keys, inp, out_size = make_batch(n, lengths, 64, seed=101 + case)
             sealed, _ = run_device(eng, torch_dev, desc, keys, inp, out_size, uniform=uniform)

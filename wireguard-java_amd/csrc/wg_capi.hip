@@ -350,8 +350,11 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
   if (!desc || (((uintptr_t)desc) & 15u)) return fail(WG_EINVAL, "descriptor array must be non-NULL and 16-byte aligned");
   if (!in || !out) return fail(WG_EINVAL, "NULL buffer");
   if (max_len > WG_MAX_PACKET) return fail(WG_E2BIG, "max_len %u > WG_MAX_PACKET", max_len);
+  // k_tile's uniform plan sizes every tile for max_len-long packets; WG_F_UNIFORM is only a
+  // scheduling hint of the transport API, so the tile kernel always plans from the lengths
   if (c->kern == KERN_TILE)
-    return launch_tiles<MODE, false>(c, desc, n, in, in_size, nullptr, 0, out, out_size, status, max_len, flags, s);
+    return launch_tiles<MODE, false>(c, desc, n, in, in_size, nullptr, 0, out, out_size, status, max_len,
+                                     flags & ~WG_F_UNIFORM, s);
   if (c->kern == KERN_WAVE1) {
     wgk::StreamParams P{};
     P.desc = desc;
