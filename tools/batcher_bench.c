@@ -79,6 +79,10 @@ int main(int argc, char** argv) {
     fprintf(stderr, "wg_ctx_create: %s\n", wg_last_error());
     return 1;
   }
+  if (getenv("WG_BENCH_KERNEL") && wg_ctx_set_kernel(g_ctx, getenv("WG_BENCH_KERNEL"), 0, 0) != WG_OK) {
+    fprintf(stderr, "wg_ctx_set_kernel: %s\n", wg_last_error());
+    return 1;
+  }
   uint8_t keys[64 * 32];
   uint64_t ks = 7;
   for (int i = 0; i < 64 * 32; ++i) keys[i] = (uint8_t)splitmix(&ks);
