@@ -80,21 +80,9 @@ int batcher_launch(Batcher* B, BatchBuf& b) {
   int rc = WG_OK;
   // seal and open entries are independent: two launches on two streams run side by side
   // (a small batch's launch is latency-bound, so this halves the batch round trip)
-#ifdef WG_BATCH_TILE  // experiment: a single packet through k_tile's uniform plan (blocks over a workgroup)
-  if (b.nseal == 1)
-    rc = launch_tiles<WG_MODE_SEAL, false>(c, b.d_sdesc, 1, b.d_in, kBatchArena, nullptr, 0, b.d_out, kBatchArena,
-                                           nullptr, b.seal_max, WG_F_UNIFORM, B->stream);
-  else
-#endif
   if (b.nseal)
     rc = launch_transport<WG_MODE_SEAL>(c, b.d_sdesc, b.nseal, b.d_in, kBatchArena, b.d_out, kBatchArena, nullptr,
                                        b.seal_max, 0, B->stream);
-#ifdef WG_BATCH_TILE
-  if (rc == WG_OK && b.nopen == 1)
-    rc = launch_tiles<WG_MODE_OPEN, false>(c, b.d_odesc, 1, b.d_in, kBatchArena, nullptr, 0, b.d_out, kBatchArena,
-                                           b.d_status, b.open_max, WG_F_UNIFORM, B->stream2);
-  else
-#endif
   if (rc == WG_OK && b.nopen)
     rc = launch_transport<WG_MODE_OPEN>(c, b.d_odesc, b.nopen, b.d_in, kBatchArena, b.d_out, kBatchArena,
                                        b.d_status, b.open_max, 0, B->stream2);
