@@ -434,6 +434,11 @@ def main():
         ok_data = bool(torch.equal(back[mask], pt[mask]))
         del idx, pkt, mask
 
+    # achievable streaming bandwidth for context: a device-to-device copy of the
+    # plaintext buffer, read + write bytes per copy time (after the check above, untimed)
+    copy_ms = train(lambda: back.copy_(pt))
+    copy_gbs = 2.0 * pt.numel() / (copy_ms * 1e-3) / 1e9
+
     payload = 2.0 * float(lengths.sum())  # sealed + opened bytes per step on this rank
     if world > 1:
         D = importlib.import_module("wireguard-java_amd.dist")
@@ -476,7 +481,8 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "alg_bytes_per_launch": int(step_alg / launches),
                          "kernel_ms": round(gpu_step_ms / launches, 5), "seal_ms": round(seal_ms, 5),
-                         "open_ms": round(open_ms, 5)},
+                         "open_ms": round(open_ms, 5), "copy_gbs": round(copy_gbs, 1),
+                         "frac_of_copy": round(achieved / copy_gbs, 4)},
             "verified": all_ok,
         }
         if valu:
