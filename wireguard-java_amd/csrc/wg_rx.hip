@@ -582,16 +582,14 @@ int wg_rx_check(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* pt, ui
     while (T < 2ull * n) T <<= 1;
     if (T > r->tab_size || (size_t)n * 4 > r->d_pos.cap)
       HIPTRY(hipDeviceSynchronize());  // the scratch is reallocated under earlier checks
-    if (T > r->tab_size) {  // (re)allocated: all entries empty (0xFF..)
+    if (T > r->tab_size) {  // (re)allocated, or reset after a failed check: all entries empty
       if ((rc = r->d_tab.ensure((size_t)T * 4)) != WG_OK) return rc;
+      if ((rc = r->d_flag.ensure(4)) != WG_OK) return rc;
       HIPTRY(hipMemsetAsync(r->d_tab.p, 0xFF, (size_t)T * 4, s));
+      HIPTRY(hipMemsetAsync(r->d_flag.p, 0, 4, s));
       r->tab_size = T;
     }
     if ((rc = r->d_pos.ensure((size_t)n * 4)) != WG_OK) return rc;
-    if (!r->d_flag.p) {
-      if ((rc = r->d_flag.ensure(4)) != WG_OK) return rc;
-      HIPTRY(hipMemsetAsync(r->d_flag.p, 0, 4, s));
-    }
     P.window = r->window;
     P.top = (uint64_t*)r->d_top.p;
     P.bits = (uint64_t*)r->d_bits.p;
@@ -605,7 +603,11 @@ int wg_rx_check(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* pt, ui
     hipLaunchKernelGGL(wgrx::k_rp_decide, dim3(grid), dim3(256), 0, s, P);
     hipLaunchKernelGGL(wgrx::k_rp_advance, dim3((c->key_slots + 255u) / 256u), dim3(256), 0, s, P);
     hipLaunchKernelGGL(wgrx::k_rp_mark, dim3(grid), dim3(256), 0, s, P);
-    HIPTRY(hipGetLastError());
+    const hipError_t le = hipGetLastError();
+    if (le != hipSuccess) {
+      r->tab_size = 0;  // the table / flag may be left dirty: the next check starts from empty ones
+      return fail(WG_EDEVICE, "replay kernels: %s", hipGetErrorString(le));
+    }
     HIPTRY(hipEventRecord(r->ev, s));
     r->ev_stream = s;
   }
