@@ -379,3 +379,58 @@ def test_set_kernel_rejects_unknown_names(engine):
     with pytest.raises(W.WgError):
         engine.set_kernel("lane", 2, 0)  # round-1 experimental kernels are no longer in the library
     engine.set_kernel("default")
+
+
+@pytest.mark.parametrize("it", range(10))
+def test_randomized_batches_vs_oracle(engine, torch_dev, it):
+    """Seeded random batches through the product kernel: random counts, lengths (some batches
+    all equal), alignments, key slots, the WG_F_UNIFORM hint either way, ~3% descriptors out
+    of range (input past the buffer, key slot past the table, len > max_len) and ~2% forged
+    tags. Seal output must equal the oracle's for the valid packets and leave the rest
+    untouched; open must report exactly the invalid and forged packets and zero-fill only
+    the forged packets' plaintexts."""
+    rng = np.random.default_rng(1000 + it)
+    n = int(rng.integers(1, 2500))
+    if it % 3 == 0:
+        lengths = np.full(n, int(rng.integers(0, 3000)), np.int64)
+    else:
+        lengths = rng.integers(0, 3000, n).astype(np.int64)
+    nkeys = int(rng.integers(1, 64))
+    desc, keys, inp, out_size = make_batch(n, lengths, nkeys, seed=2000 + it,
+                                           in_align=int(rng.choice([1, 4, 16])), out_pad=int(rng.choice([0, 3, 16])))
+    desc["in_off"] += np.uint64(int(rng.integers(0, 4)))
+    max_len = int(lengths.max())
+    bad = rng.random(n) < 0.03
+    kind = rng.integers(0, 3, n)
+    for i in np.nonzero(bad)[0]:
+        if kind[i] == 0:
+            desc["in_off"][i] = len(inp) + 7
+        elif kind[i] == 1:
+            desc["key_slot"][i] = engine.key_slots + 3
+        else:
+            desc["len"][i] = max_len + 1
+    uniform = bool(rng.integers(0, 2))
+    sealed, _ = run_device(engine, torch_dev, desc, keys, inp, out_size, uniform=uniform, max_len=max_len)
+    ref = np.zeros(out_size, np.uint8)
+    good = np.nonzero(~bad)[0]
+    if len(good):
+        O.seal_batch(desc[good], inp, ref, keys, threads=8)
+    assert np.array_equal(sealed, ref), it
+    # open: ciphertext back to plaintext; forge ~2% of the valid packets' tags
+    od = desc.copy()
+    od["in_off"], od["out_off"] = desc["out_off"], desc["in_off"]
+    forged = (~bad) & (rng.random(n) < 0.02)
+    ct = sealed.copy()
+    for i in np.nonzero(forged)[0]:
+        ct[int(od["in_off"][i]) + int(od["len"][i])] ^= 0x80
+    for i in np.nonzero(bad & (kind == 0))[0]:
+        od["in_off"][i] = out_size + 7  # still out of range on the open side
+    pt, st = run_device(engine, torch_dev, od, keys, ct, len(inp), open_=True, uniform=uniform, max_len=max_len)
+    exp = (bad | forged).astype(np.int32)
+    assert np.array_equal(st, exp), it
+    for i in range(n):
+        if bad[i]:
+            continue
+        o, L_ = int(desc["in_off"][i]), int(desc["len"][i])
+        want = np.zeros(L_, np.uint8) if forged[i] else inp[o:o + L_]
+        assert np.array_equal(pt[o:o + L_], want), (it, i)
