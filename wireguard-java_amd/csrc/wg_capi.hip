@@ -313,13 +313,11 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   const uint32_t waves = (uint32_t)((n + 8ull * per_slot - 1) / (8ull * per_slot));
   const uint32_t grid = (waves + wgt::TW - 1) / wgt::TW;
   P.slots = grid * wgt::TW * 8u;
-  // rounds a slot runs, spread over the 4 issue-priority levels (k_transport)
+  // mixed lengths: the rounds a slot runs, spread over the 4 issue-priority levels (k_transport),
+  // so the waves that have done the least work issue first (C2 +2%); uniform batches keep the
+  // default oldest-first arbitration (the same schedule cost C1 2%)
   const uint32_t max_rounds = (host_pkt_blocks<WG_MODE_SEAL>(max_len) + 7u) / 8u;
-#ifndef WG_PRIO
-  P.prio_step = 0;
-#else
-  P.prio_step = std::max<uint32_t>(1u, (uint32_t)((per_slot * max_rounds + 3u) / 4u));
-#endif
+  P.prio_step = (flags & WG_F_UNIFORM) ? 0u : std::max<uint32_t>(1u, (uint32_t)((per_slot * max_rounds + 3u) / 4u));
   if (!(flags & WG_F_UNIFORM) && per_slot > 1) {  // longest-first order (LPT) for the snake
     int rc;
     const uint32_t lgrid = std::max<uint32_t>(1u, std::min<uint32_t>(wgt::LPT_MAX_BLOCKS, (n + 1023u) / 1024u));

@@ -269,11 +269,11 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
   // lane j of a slot holds the packet's first-round column (j & 3) (a, b, c, d); lanes 1..3
   // feed the other lanes' blocks through ds_swizzle broadcasts
   uint32_t hc[4] = {0u, 0u, 0u, 0u};
-  // Progress-based issue priority (off: prio_step = 0 unless built with WG_PRIO): a SIMD
+  // Progress-based issue priority (mixed-length batches; prio_step = 0 for uniform ones): a SIMD
   // arbitrates VALU issue by priority, then age, so with equal priorities the oldest of its 8
   // waves runs ahead and the waves finish one after another. A wave drops one priority level
   // every prio_step rounds instead, so the waves that have done the least work issue first
-  // (measured: no change on C1).
+  // (C2 +2%, C1 -2%: DESIGN.md §4.2).
   uint32_t iter = 0;  // wave-uniform
   WG_PH_DECL
   while (true) {
