@@ -520,7 +520,8 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
 #else
             uint4 v = make_uint4(acc[0] ^ t, acc[1], acc[2] + c0, acc[3]);
 #endif
-            poly_mul_ilp(acc, R, Rs);
+            // acc is still 0 before a packet's first chunk (round 0, t = 0): no product needed
+            if (round != 0 || t != 0) poly_mul_ilp(acc, R, Rs);
             uint32_t cl[5];
             poly_block_limbs(v.x, v.y, v.z, v.w, 1u << 24, cl);
 #pragma unroll
