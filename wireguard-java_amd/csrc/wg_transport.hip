@@ -692,12 +692,29 @@ __global__ void __launch_bounds__(LPT_THREADS) k_lpt_scatter(const wg_pkt* d, ui
     base[k] = before;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {  // packets with a larger key come first
-    uint32_t acc = 0;
-    for (int k = (int)LPT_BINS - 1; k >= 0; --k) {
-      const uint32_t c = tot[k];
-      tot[k] = acc;
-      acc += c;
+  if (threadIdx.x < 64u) {  // packets with a larger key come first: wave 0 scans the keys
+    // in descending order, lane l holding positions 3l..3l+2 (key LPT_BINS-1-p)
+    static_assert(3u * 64u >= LPT_BINS, "three keys per lane");
+    const uint32_t l = threadIdx.x;
+    uint32_t v[3], own = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 3u; ++q) {
+      const uint32_t p = 3u * l + q;
+      v[q] = p < LPT_BINS ? tot[LPT_BINS - 1u - p] : 0u;
+      own += v[q];
+    }
+    uint32_t inc = own;
+#pragma unroll
+    for (uint32_t off = 1; off < 64u; off <<= 1) {
+      const uint32_t up = __shfl_up(inc, off, 64);
+      inc += l >= off ? up : 0u;
+    }
+    uint32_t acc = inc - own;
+#pragma unroll
+    for (uint32_t q = 0; q < 3u; ++q) {
+      const uint32_t p = 3u * l + q;
+      if (p < LPT_BINS) tot[LPT_BINS - 1u - p] = acc;
+      acc += v[q];
     }
   }
   __syncthreads();
