@@ -16,7 +16,7 @@ echo "[round] smoke"; timeout -k 10 300 python -c "import __graft_entry__ as g; 
 tail -1 $O/smoke.log
 echo "[round] bench c1"; timeout -k 10 400 python bench.py > $O/bench_c1.json 2> $O/bench.err
 cat $O/bench_c1.json
-echo "[round] bench c2"; timeout -k 10 300 python bench.py --workload c2 --no-cpu-baseline > $O/bench_c2.json 2>> $O/bench.err
+echo "[round] bench c2"; timeout -k 10 300 python bench.py --workload c2 > $O/bench_c2.json 2>> $O/bench.err
 cat $O/bench_c2.json
 if [ "$2" != "quick" ]; then
   echo "[round] bench c3"; timeout -k 10 400 python bench.py --workload c3 --no-cpu-baseline --steps 5 --warmup 1 > $O/bench_c3.json 2>> $O/bench.err
