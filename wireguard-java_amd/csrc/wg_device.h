@@ -12,6 +12,10 @@
 // ~30 T. The rotates therefore set the ChaCha20 cost; 16/8-bit rotates use
 // v_perm_b32 (measured 1-3% ahead of v_alignbit_b32).
 #pragma once
+
+#ifndef WG_CHACHA_UNROLL
+#define WG_CHACHA_UNROLL 3  // double rounds per loop trip of chacha20_block_hoisted (9 in all)
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -108,7 +112,7 @@ __device__ __forceinline__ void chacha20_block_hoisted(const uint4* key_lds, uin
   uint32_t x3 = H[8], x7 = H[9], x11 = H[10], x15 = H[11];
   WG_QR(x0, x4, x8, x12)
   WG_QR(x0, x5, x10, x15) WG_QR(x1, x6, x11, x12) WG_QR(x2, x7, x8, x13) WG_QR(x3, x4, x9, x14)
-#pragma unroll 3
+#pragma unroll WG_CHACHA_UNROLL
   for (int r = 1; r < 10; ++r) {
     WG_QR(x0, x4, x8, x12) WG_QR(x1, x5, x9, x13) WG_QR(x2, x6, x10, x14) WG_QR(x3, x7, x11, x15)
     WG_QR(x0, x5, x10, x15) WG_QR(x1, x6, x11, x12) WG_QR(x2, x7, x8, x13) WG_QR(x3, x4, x9, x14)
