@@ -261,8 +261,11 @@ def launch_check(args):
     t0 = time.perf_counter()
     time.sleep(0.01 * (rank + 1))
     elapsed = time.perf_counter() - t0
+    D = importlib.import_module("wireguard-java_amd.dist")
+    per_gpu = D.gather_per_rank(dist if world > 1 else None, "cpu", {
+        "elapsed_s": elapsed, "payload_bytes": 1000.0 * (rank + 1), "packets": 10 * (rank + 1), "seal_ms": 0.0,
+        "open_ms": 0.0, "kernel_ms": 0.0})
     if world > 1:
-        D = importlib.import_module("wireguard-java_amd.dist")
         (elapsed,), payload, ok = D.reduce_report(dist, "cpu", [elapsed], 1000.0 * (rank + 1), True)
         dist.barrier()
         dist.destroy_process_group()
@@ -270,7 +273,7 @@ def launch_check(args):
         payload, ok = 1000.0, True
     if rank == 0:
         print(json.dumps({"launch_check": True, "n_gpus": world, "elapsed_max": elapsed,
-                          "payload_sum": payload, "ok": ok}), flush=True)
+                          "payload_sum": payload, "ok": ok, "per_gpu": per_gpu}), flush=True)
     return 0
 
 
@@ -440,8 +443,14 @@ def main():
     copy_gbs = 2.0 * pt.numel() / (copy_ms * 1e-3) / 1e9
 
     payload = 2.0 * float(lengths.sum())  # sealed + opened bytes per step on this rank
+    D = importlib.import_module("wireguard-java_amd.dist")
+    launches = 1 if args.mode == "duplex" else 2  # kernel launches per step
+    # this rank's own figures, gathered before the max-over-ranks reduction (BASELINE configs[3]:
+    # per-GPU and aggregate GiB/s)
+    per_gpu = D.gather_per_rank(dist if world > 1 else None, dev, {
+        "elapsed_s": elapsed, "payload_bytes": payload * args.steps, "packets": n, "seal_ms": seal_ms,
+        "open_ms": open_ms, "kernel_ms": gpu_step_ms / launches})
     if world > 1:
-        D = importlib.import_module("wireguard-java_amd.dist")
         (elapsed, seal_ms, open_ms, gpu_step_ms), payload_all, all_ok = D.reduce_report(
             dist, dev, [elapsed, seal_ms, open_ms, gpu_step_ms], payload, ok_status and ok_data)
     else:
@@ -455,7 +464,6 @@ def main():
     traffic = pmc_traffic(args.mode) if args.workload == "c1" else None
     valu = pmc_valu_insts(args.mode) if args.workload == "c1" else None
 
-    launches = 1 if args.mode == "duplex" else 2  # kernel launches per step
     if args.mode == "duplex":
         kname = "k_duplex (seal + open halves)"
     else:
@@ -484,6 +492,9 @@ def main():
                          "open_ms": round(open_ms, 5), "copy_gbs": round(copy_gbs, 1),
                          "frac_of_copy": round(achieved / copy_gbs, 4)},
             "verified": all_ok,
+            "per_gpu": [{"rank": r["rank"], "gib_s": round(r["gib_s"], 2), "packets_per_step": r["packets"],
+                         "elapsed_s": round(r["elapsed_s"], 6), "seal_ms": round(r["seal_ms"], 5),
+                         "open_ms": round(r["open_ms"], 5), "kernel_ms": round(r["kernel_ms"], 5)} for r in per_gpu],
         }
         if valu:
             rate = valu / (gpu_step_ms / launches * 1e-3)

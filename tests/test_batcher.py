@@ -1,8 +1,10 @@
-"""Per-packet wg_seal1 / wg_open1 through the batcher (realised under the
-unchanged per-packet API): many threads call concurrently, as the reference's ForkJoinPool
-workers call SymmetricKeypair.cipher / decipher (TransportManager.java:41,79,152-158);
-their packets share device launches, and every result is bit-exact vs the oracle."""
+"""Per-packet wg_seal1 / wg_open1 through the persistent per-packet server k_pp (SURVEY §8f
+rank 1, realised under the unchanged per-packet API): many threads call concurrently, as the
+reference's ForkJoinPool workers call SymmetricKeypair.cipher / decipher
+(TransportManager.java:41,79,152-158); one resident kernel serves all of them without a launch
+per packet, and every result is bit-exact vs the oracle."""
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -52,20 +54,21 @@ def test_sixteen_threads_mixed_seal_open_bit_exact():
         assert not errors, errors[:3]
         launches, packets = eng.batcher_stats()
         assert packets == T * N
-        assert launches < packets  # concurrent callers shared launches
+        assert launches < packets  # one resident kernel served many packets
     finally:
         eng.close()
 
 
 @pytest.mark.gpu
 def test_keypair_api_through_batcher_with_window():
-    """SymmetricKeypair.cipher / decipher (the unchanged reference API) on two threads with
-    an accumulation window configured; counters are claimed atomically (getAndAdd, :64)."""
+    """SymmetricKeypair.cipher / decipher (the unchanged reference API) on two threads with a
+    4-wave server that goes idle after 200 us (so it exits and is relaunched between bursts);
+    counters are claimed atomically (getAndAdd, :64)."""
     n = __import__("wgtest").noise()
     W = wg()
     eng = W.Engine(0, key_slots=8)
     try:
-        eng.batcher_config(max_batch=256, window_us=50)
+        eng.batcher_config(waves=4, idle_us=200)
         k1, k2 = splitmix_bytes(1701, 32), splitmix_bytes(1702, 32)
         a = n.SymmetricKeypair(k1, k2, engine=eng)
         b = n.SymmetricKeypair(k2, k1, engine=eng)
@@ -83,6 +86,8 @@ def test_keypair_api_through_batcher_with_window():
                 assert bytes(dst) == O.c_aead_seal(k1, O.transport_nonce(c), pt)
                 with lock:
                     used.append(c)
+                if i % 50 == 49:
+                    time.sleep(0.002)  # let the server go idle and exit
 
         th = [threading.Thread(target=send, args=(t,)) for t in range(2)]
         for x in th:
@@ -91,6 +96,65 @@ def test_keypair_api_through_batcher_with_window():
             x.join()
         assert sorted(used) == list(range(600))
         a.clean(); b.clean()
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_per_packet_edges_bit_exact():
+    """Keepalive (0 B), the largest slot packet (4080 B), packets past a slot (4081, 9000,
+    65535 B: the host batch path), a key change and wg_keys_zero between calls, and a forged
+    tag that must leave the caller's buffer untouched (ChaCha20Poly1305.java:51-55)."""
+    import ctypes
+    W = wg()
+    eng = W.Engine(0, key_slots=4)
+    try:
+        keys = splitmix_np(1801, 32 * 4)
+        eng.set_keys(0, keys.tobytes())
+        for L in (0, 1, 15, 16, 17, 63, 64, 65, 1420, 2032, 4080, 4081, 9000, 65535):
+            for slot in (0, 3):
+                key = keys[32 * slot:32 * slot + 32].tobytes()
+                ctr = (L << 20) | slot
+                pt = splitmix_bytes(L * 7 + slot, L)
+                want = O.c_aead_seal(key, O.transport_nonce(ctr), pt)
+                assert eng.seal1(slot, ctr, pt) == want, L
+                assert eng.open1(slot, ctr, want) == pt, L
+        # rekey slot 1, then zero it: the next calls use the new / zero key
+        k_new = splitmix_bytes(1802, 32)
+        eng.set_keys(1, k_new)
+        pt = splitmix_bytes(1803, 700)
+        assert eng.seal1(1, 5, pt) == O.c_aead_seal(k_new, O.transport_nonce(5), pt)
+        eng.zero_keys(1, 1)
+        assert eng.seal1(1, 6, pt) == O.c_aead_seal(bytes(32), O.transport_nonce(6), pt)
+        # forged tag: return 1, dst untouched
+        lib = W.lib()
+        for L in (100, 5000):
+            key = keys[:32].tobytes()
+            sealed = bytearray(O.c_aead_seal(key, O.transport_nonce(9), splitmix_bytes(L, L)))
+            sealed[L + 3] ^= 1
+            src = (ctypes.c_uint8 * len(sealed)).from_buffer_copy(bytes(sealed))
+            dst = (ctypes.c_uint8 * L)(*([0xA5] * L))
+            assert lib.wg_open1(eng.ctx, 0, 9, src, L, dst) == 1
+            assert bytes(dst) == b"\xa5" * L
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_failed_server_launch_is_not_sticky(monkeypatch):
+    """A failed launch of the per-packet server fails only the call that hit it; the next
+    call launches again and succeeds (test hook WG_PP_TEST_FAIL_LAUNCHES)."""
+    monkeypatch.setenv("WG_PP_TEST_FAIL_LAUNCHES", "1")
+    W = wg()
+    eng = W.Engine(0, key_slots=1)
+    try:
+        key = splitmix_bytes(1901, 32)
+        eng.set_keys(0, key)
+        pt = splitmix_bytes(1902, 300)
+        with pytest.raises(W.WgError):
+            eng.seal1(0, 1, pt)
+        assert eng.seal1(0, 2, pt) == O.c_aead_seal(key, O.transport_nonce(2), pt)
+        assert eng.seal1(0, 3, pt) == O.c_aead_seal(key, O.transport_nonce(3), pt)
     finally:
         eng.close()
 

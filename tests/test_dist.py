@@ -126,6 +126,13 @@ def test_bench_spawns_ranks_without_torchrun():
     assert out["n_gpus"] == 2 and out["ok"]
     assert out["payload_sum"] == 3000.0          # 1000 (rank 0) + 2000 (rank 1)
     assert out["elapsed_max"] >= 0.019           # rank 1 sleeps 20 ms: the max, not rank 0's
+    per = out["per_gpu"]                         # each rank's own figures, in rank order
+    assert [r["rank"] for r in per] == [0, 1]
+    assert sum(r["payload_bytes"] for r in per) == out["payload_sum"]
+    assert [r["packets"] for r in per] == [10, 20]
+    assert per[1]["elapsed_s"] == out["elapsed_max"] and per[0]["elapsed_s"] < per[1]["elapsed_s"]
+    for r in per:
+        assert abs(r["gib_s"] - r["payload_bytes"] / r["elapsed_s"] / 2**30) < 1e-12
 
 
 def test_bench_rejects_world_size_mismatch():

@@ -75,7 +75,8 @@ struct DevBuf {
 // transport kernels selectable per context (wg_ctx_set_kernel)
 enum Kern { KERN_TRANSPORT = 0, KERN_WAVE1 = 1, KERN_TILE = 2 };
 
-struct Batcher;  // wg_batcher.hip
+struct PPServer;  // wg_pp.hip
+void pp_stop(wg_ctx* c);
 struct RxState;  // wg_rx.hip
 
 }  // namespace
@@ -99,8 +100,10 @@ struct wg_ctx {
   // host-API staging
   DevBuf h_desc, h_in, h_out, h_aad, h_status, h_keys;
   std::mutex mu;  // serialises host-API calls and plan workspace reuse
-  Batcher* batcher = nullptr;
-  std::mutex batcher_mu;
+  PPServer* pp = nullptr;  // persistent per-packet server (wg_seal1 / wg_open1)
+  std::mutex pp_mu;
+  std::vector<uint8_t> keys_host;  // host mirror of the key table: the per-packet path sends keys with the packet
+  std::mutex keys_mu;
   RxState* rx = nullptr;  // receive-side checks (wg_rx.hip)
   // timing
   bool timing = false;
@@ -394,7 +397,6 @@ hipStream_t pick_stream(wg_ctx*, void* stream) { return (hipStream_t)stream; }
 
 }  // namespace
 
-#include "wg_batcher.hip"
 #include "wg_rx.hip"
 
 extern "C" {
@@ -455,6 +457,7 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
     wg_ctx_destroy(c);
     return fail(WG_ENOMEM, "context allocation failed on device %d", device);
   }
+  c->keys_host.assign((size_t)key_slots * 32, 0);
   c->resident_waves[0] = (uint32_t)std::max(bps, 1) * wgt::TW * (uint32_t)prop.multiProcessorCount;
   c->resident_waves[1] = (uint32_t)std::max(bpo, 1) * wgt::TW * (uint32_t)prop.multiProcessorCount;
   *out = c;
@@ -463,7 +466,8 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
 
 int wg_ctx_destroy(wg_ctx* c) {
   if (!c) return WG_OK;
-  batcher_stop(c);
+  pp_stop(c);
+  std::fill(c->keys_host.begin(), c->keys_host.end(), (uint8_t)0);
   DeviceGuard g(c->device);
   rx_free(c);
   if (c->keys) {
@@ -503,7 +507,12 @@ int wg_keys_set(wg_ctx* c, uint32_t first, uint32_t n, const uint8_t* keys_host)
   if ((uint64_t)first + n > c->key_slots) return fail(WG_ERANGE, "key slots [%u, %u) exceed table of %u", first, first + n, c->key_slots);
   if (!n) return WG_OK;
   DeviceGuard g(c->device);
+  std::lock_guard<std::mutex> lk(c->mu);  // the replay-window reset is ordered with queued checks under it
   HIPTRY(hipMemcpyAsync((uint8_t*)c->keys + (size_t)first * 32, keys_host, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+  {
+    std::lock_guard<std::mutex> lk2(c->keys_mu);
+    memcpy(c->keys_host.data() + (size_t)first * 32, keys_host, (size_t)n * 32);
+  }
   int rc;
   if ((rc = rx_reset_slots(c, first, n, c->stream)) != WG_OK) return rc;  // new key: new session
   HIPTRY(hipStreamSynchronize(c->stream));
@@ -515,7 +524,12 @@ int wg_keys_zero(wg_ctx* c, uint32_t first, uint32_t n) {
   if ((uint64_t)first + n > c->key_slots) return fail(WG_ERANGE, "key slots out of range");
   if (!n) return WG_OK;
   DeviceGuard g(c->device);
+  std::lock_guard<std::mutex> lk(c->mu);
   HIPTRY(hipMemsetAsync((uint8_t*)c->keys + (size_t)first * 32, 0, (size_t)n * 32, c->stream));
+  {
+    std::lock_guard<std::mutex> lk2(c->keys_mu);
+    memset(c->keys_host.data() + (size_t)first * 32, 0, (size_t)n * 32);
+  }
   int rc;
   if ((rc = rx_reset_slots(c, first, n, c->stream)) != WG_OK) return rc;
   HIPTRY(hipStreamSynchronize(c->stream));
@@ -678,6 +692,7 @@ int wg_aead_batch(wg_ctx* c, int mode, const wg_aead_desc* desc, uint32_t n, con
 }  // extern "C"
 
 #include "wg_host.hip"
+#include "wg_pp.hip"
 
 extern "C" {
 

@@ -99,6 +99,52 @@ __device__ __forceinline__ void chacha20_block_lds(const uint4* key_lds, uint32_
 // One ChaCha20 column quarter round on its own (the per-packet part of the first round).
 __device__ __forceinline__ void chacha20_qr(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) { WG_QR(a, b, c, d) }
 
+// ---- ChaCha20 rounds as placed VOP3 code (gfx950 issue rate) ---------------------------
+// Measured on MI355X (tools/microbench16-18): a ChaCha20 double round issues
+// at 3.9-4.1 cycles per wave-instruction (8 waves per SIMD) as the compiler emits it (4-byte
+// VOP2 v_add/v_xor mixed with 8-byte v_alignbit), and at 3.35-3.48 when EVERY instruction is
+// an 8-byte VOP3 encoding placed at an address = 4 mod 8 (the same stream at 0 mod 8: 4.0).
+// So the rounds are one asm block of _e64 encodings, started by `.p2align 3; s_nop 0` (the
+// nop executes once per block). Operands %0..%15 are state words x0..x15; the order inside a
+// step is grouped (the four columns' adds, then xors, then rotates), rotl(x, n) =
+// v_alignbit(x, x, 32 - n).
+#define WG_A(a, b) "v_add_u32_e64 %" #a ", %" #a ", %" #b "\n"
+#define WG_X(d, a) "v_xor_b32_e64 %" #d ", %" #d ", %" #a "\n"
+#define WG_R(d, s) "v_alignbit_b32 %" #d ", %" #d ", %" #d ", " #s "\n"
+#define WG_STEP4(p0, q0, t0, p1, q1, t1, p2, q2, t2, p3, q3, t3, s)                         \
+  WG_A(p0, q0) WG_A(p1, q1) WG_A(p2, q2) WG_A(p3, q3) WG_X(t0, p0) WG_X(t1, p1) WG_X(t2, p2) \
+  WG_X(t3, p3) WG_R(t0, s) WG_R(t1, s) WG_R(t2, s) WG_R(t3, s)
+// four quarter rounds (a_i, b_i, c_i, d_i), i = 0..3, interleaved step by step
+#define WG_QR4(a0, b0, c0, d0, a1, b1, c1, d1, a2, b2, c2, d2, a3, b3, c3, d3)     \
+  WG_STEP4(a0, b0, d0, a1, b1, d1, a2, b2, d2, a3, b3, d3, 16)                     \
+  WG_STEP4(c0, d0, b0, c1, d1, b1, c2, d2, b2, c3, d3, b3, 20)                     \
+  WG_STEP4(a0, b0, d0, a1, b1, d1, a2, b2, d2, a3, b3, d3, 24)                     \
+  WG_STEP4(c0, d0, b0, c1, d1, b1, c2, d2, b2, c3, d3, b3, 25)
+#define WG_QR1(a, b, c, d)                                                                  \
+  WG_A(a, b) WG_X(d, a) WG_R(d, 16) WG_A(c, d) WG_X(b, c) WG_R(b, 20) WG_A(a, b) WG_X(d, a) \
+  WG_R(d, 24) WG_A(c, d) WG_X(b, c) WG_R(b, 25)
+#define WG_COLS WG_QR4(0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15)
+#define WG_DIAGS WG_QR4(0, 5, 10, 15, 1, 6, 11, 12, 2, 7, 8, 13, 3, 4, 9, 14)
+#define WG_DR WG_COLS WG_DIAGS
+#define WG_PLACE ".p2align 3\ns_nop 0\n"
+#define WG_X16(x)                                                                                       \
+  "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),       \
+      "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15])
+
+// the 20 rounds of chacha_permute (chacha-generic.c:10-55) on x[0..15]
+__device__ __forceinline__ void chacha20_rounds_asm(uint32_t x[16]) {
+  asm volatile(WG_PLACE WG_DR WG_DR WG_DR WG_DR WG_DR WG_DR WG_DR WG_DR WG_DR WG_DR : WG_X16(x));
+}
+// the same with columns 1..3 of the first column round already applied (chacha20_block_hoisted)
+__device__ __forceinline__ void chacha20_rounds_hoisted_asm(uint32_t x[16]) {
+  asm volatile(WG_PLACE WG_QR1(0, 4, 8, 12) WG_DIAGS WG_DR WG_DR WG_DR WG_DR WG_DR WG_DR WG_DR WG_DR WG_DR
+               : WG_X16(x));
+}
+
+#ifndef WG_CHACHA_ASM
+#define WG_CHACHA_ASM 1
+#endif
+
 // Same block with the first column round of columns 1..3 already done: they depend only on
 // the key and the nonce (state words 13..15), not on the block counter, so a packet computes
 // them once (H = {x1, x5, x9, x13, x2, x6, x10, x14, x3, x7, x11, x15} after that round)
@@ -106,6 +152,19 @@ __device__ __forceinline__ void chacha20_qr(uint32_t& a, uint32_t& b, uint32_t& 
 __device__ __forceinline__ void chacha20_block_hoisted(const uint4* key_lds, uint32_t ctr, uint32_t n0, uint32_t n1,
                                                        uint32_t n2, const uint32_t H[12], uint32_t out[16]) {
   uint4 ka = key_lds[0], kb = key_lds[1];
+#if WG_CHACHA_ASM
+  uint32_t y[16] = {0x61707865u, H[0], H[4], H[8], ka.x, H[1], H[5], H[9],
+                    kb.x,        H[2], H[6], H[10], ctr, H[3], H[7], H[11]};
+  chacha20_rounds_hoisted_asm(y);
+  asm volatile("" ::: "memory");
+  ka = key_lds[0];
+  kb = key_lds[1];
+  out[0] = y[0] + 0x61707865u; out[1] = y[1] + 0x3320646eu; out[2] = y[2] + 0x79622d32u; out[3] = y[3] + 0x6b206574u;
+  out[4] = y[4] + ka.x; out[5] = y[5] + ka.y; out[6] = y[6] + ka.z; out[7] = y[7] + ka.w;
+  out[8] = y[8] + kb.x; out[9] = y[9] + kb.y; out[10] = y[10] + kb.z; out[11] = y[11] + kb.w;
+  out[12] = y[12] + ctr; out[13] = y[13] + n0; out[14] = y[14] + n1; out[15] = y[15] + n2;
+  return;
+#endif
   uint32_t x0 = 0x61707865u, x4 = ka.x, x8 = kb.x, x12 = ctr;
   uint32_t x1 = H[0], x5 = H[1], x9 = H[2], x13 = H[3];
   uint32_t x2 = H[4], x6 = H[5], x10 = H[6], x14 = H[7];

@@ -1,0 +1,545 @@
+// wg_pp.hip — the per-packet entry points wg_seal1 / wg_open1 served by a persistent
+// device kernel (included by wg_capi.hip).
+//
+// The reference seals / opens one packet per synchronous call from ForkJoinPool workers
+// (TransportManager.java:41,79,152-158 -> SymmetricKeypair.java:63-83). Those calls stay
+// per-packet and synchronous. Round 2 batched them under a launcher thread (one kernel
+// launch per batch, ~35 us per round trip, 0.2 GiB/s at 16 callers); here a small
+// persistent kernel (k_pp, W one-wave workgroups) serves them through pinned memory with
+// no launch on the per-packet path:
+//   caller: ticket t (atomic), entry i = t mod kRing; copy the packet + header {mode, len,
+//           counter, key} into in-slot i (pinned, fine-grained host memory), then publish
+//           seq = t + 1 in the slot header (release store, after every other byte);
+//   wave t mod W: polls seq of its next ticket (one system-scope load over PCIe), reads the
+//           header and payload (coalesced system-scope loads into LDS), runs the whole
+//           packet with its 64 lanes (lane j = ChaCha20 block j; 64-strided Poly1305
+//           Horner over the LDS image with r^64, r-power scan across the wave), writes
+//           ct||tag / plaintext into out-slot i (system-scope stores), waits for them,
+//           then stores done[i] = (t + 1) << 8 | status;
+//   caller: spins on done[i] in its own memory, copies the result out (open: only when the
+//           tag verified, so dst stays untouched on a bad tag, ChaCha20Poly1305.java:51-55).
+// The session key travels in the slot header from a host mirror of the key table (the
+// reference keeps its keys in host memory too, SymmetricKeypair.java:40-50), so the
+// persistent kernel never reads a device key table that wg_keys_set may rewrite under it.
+// Exit conditions every wave reaches: the context's stop flag, no work for idle_us, or a
+// lifetime of life_ms (then the next caller relaunches). Packets longer than a slot
+// (> kPPMaxLen, beyond the reference pipeline's 4-KB buffers) take the host batch path.
+#pragma once
+
+namespace wgpp {
+
+using namespace wgd;
+using wgt::mask_chunk;
+
+constexpr uint32_t kRing = 512;                 // entries (concurrent per-packet calls)
+constexpr uint32_t kHdr = 64;                   // in-slot header bytes
+constexpr uint32_t kData = 4096;                // payload bytes per slot
+constexpr uint32_t kInSlot = kHdr + kData;      // in-slot stride
+constexpr uint32_t kOutSlot = kData;            // out-slot stride
+constexpr uint32_t kPPMaxLen = kData - 16;      // 4080: payload + tag fit a slot
+constexpr uint32_t kMaxWaves = 64;
+
+struct Hdr {          // first 64 B of an in-slot (host-written)
+  uint64_t seq;       // ticket + 1: written last
+  uint64_t counter;   // transport counter (nonce = LE64(counter) || 0^4)
+  uint32_t mode;      // WG_MODE_SEAL / WG_MODE_OPEN
+  uint32_t len;       // payload bytes (open: ct, the tag follows)
+  uint32_t key[8];
+  uint32_t _pad[2];
+};
+static_assert(sizeof(Hdr) == kHdr, "slot header is 64 B");
+
+struct Ctl {          // pinned, host-written
+  uint32_t stop;
+  uint32_t _pad[15];
+};
+
+struct PPParams {
+  const uint8_t* in;      // device alias: kRing in-slots
+  uint8_t* out;           // device alias: kRing out-slots
+  uint64_t* done;         // device alias: kRing completion words
+  const Ctl* ctl;         // device alias
+  uint64_t* exit_flag;    // device alias (pinned): gen, written by the last wave to exit
+  uint64_t* next;         // device memory: next ticket per wave (kept across launches)
+  uint32_t* exited;       // device memory: waves exited in this launch (zeroed before it)
+  uint32_t waves;
+  uint32_t gen;
+  uint64_t idle_ticks;    // s_memrealtime ticks (100 MHz)
+  uint64_t life_ticks;
+};
+
+__device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld_sys64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+#ifdef WG_PP_STAMPS  // tools/pp_stamps.hip only: s_memrealtime per phase of each ticket
+__device__ uint64_t g_pp_stamps[4096][8];
+#define PP_STAMP(t, k) \
+  if ((threadIdx.x & 63u) == 0) g_pp_stamps[(t) % 4096u][k] = __builtin_amdgcn_s_memrealtime()
+#else
+#define PP_STAMP(t, k) do {} while (0)
+#endif
+
+// Dwords of an in-slot read right after its seq is seen: the header and the first 1472 payload
+// bytes in one round trip over PCIe (6 coalesced wave loads); longer packets read the rest next.
+constexpr uint32_t kFirstDw = 384;
+
+// One packet by one wave. img_in: payload (+ tag) as read; img_out: the result. Both also
+// serve as the MAC image (seal: the ciphertext in img_out; open: the ciphertext in img_in).
+__device__ void pp_packet(const Hdr& h, uint64_t ticket, const uint8_t* slot, uint8_t* out, uint64_t* done,
+                          uint4* img_in, uint4* img_out) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool open = h.mode == WG_MODE_OPEN;
+  const uint32_t len = h.len;
+  const uint32_t n_in = len + (open ? 16u : 0u);
+  {  // the rest of the payload (img_in follows the header in the same LDS image)
+    const uint4* src = (const uint4*)slot;
+    uint4* dst = img_in - kHdr / 16;
+    const uint32_t nq = kHdr / 16 + ((n_in + 15u) >> 4);
+    for (uint32_t k = kFirstDw / 4 + lane; k < nq; k += 64u) dst[k] = src[k];
+  }
+  // open: the received tag, before the MAC image masks it
+  uint32_t tag_in = 0;
+  lds_sync();
+  PP_STAMP(ticket, 2);
+  if (open && lane < 16u) tag_in = ((const uint8_t*)img_in)[len + lane];
+  lds_sync();
+
+  const uint32_t nc = (len + 15u) >> 4;          // ciphertext chunks
+  const uint32_t nb = ((len + 63u) >> 6) + 1u;   // ChaCha20 blocks incl. the key block
+  uint32_t pk[8] = {0, 0, 0, 0, 0, 0, 0, 0};     // Poly1305 one-time key (block 0)
+  uint4* mac = open ? img_in : img_out;
+  for (uint32_t r = 0; r * 64u < nb; ++r) {
+    const uint32_t b = 64u * r + lane;
+    uint32_t x[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, h.key[0], h.key[1], h.key[2], h.key[3],
+                      h.key[4],    h.key[5],    h.key[6],    h.key[7],    b,        (uint32_t)h.counter,
+                      (uint32_t)(h.counter >> 32), 0u};
+    chacha20_rounds_asm(x);
+    const uint32_t st[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, h.key[0], h.key[1], h.key[2], h.key[3],
+                             h.key[4],    h.key[5],    h.key[6],    h.key[7],    b,        (uint32_t)h.counter,
+                             (uint32_t)(h.counter >> 32), 0u};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] += st[i];
+    if (r == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) pk[i] = __builtin_amdgcn_readfirstlane(x[i]);  // lane 0 = block 0
+    }
+    if (b >= 1u && b < nb) {
+#pragma unroll
+      for (uint32_t q = 0; q < 4u; ++q) {
+        const uint32_t c = 4u * (b - 1u) + q;  // chunk index
+        if (c < nc) {
+          const uint32_t cb = min(16u, len - 16u * c);
+          uint4 v = img_in[c];
+          if (cb < 16u) v = mask_chunk(v, cb);
+          uint4 o = make_uint4(x[4 * q] ^ v.x, x[4 * q + 1] ^ v.y, x[4 * q + 2] ^ v.z, x[4 * q + 3] ^ v.w);
+          if (cb < 16u) o = mask_chunk(o, cb);
+          img_out[c] = o;
+          if (open && cb < 16u) img_in[c] = v;  // MAC input: the zero-padded ciphertext
+        }
+      }
+    }
+  }
+  lds_sync();
+  PP_STAMP(ticket, 3);
+  if (lane == 0) mac[nc] = make_uint4(0u, 0u, len, 0u);  // le64(aad len = 0) || le64(len)
+  lds_sync();
+
+  // Poly1305 over M = nc + 1 chunks: front padding D so lane j holds positions j + 64 t,
+  // acc_j = sum_t m(j + 64 t) R^(T-1-t) with R = r^64; tag poly = sum_j acc_j r^(64 - j)
+  uint32_t y[5];
+  poly_r_limbs(pk[0], pk[1], pk[2], pk[3], y);
+#pragma unroll
+  for (uint32_t s = 1; s < 64u; s <<= 1) {  // lane j: r^(j+1)
+    uint32_t z[5], zs[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) z[i] = (uint32_t)__shfl_up((int)y[i], s, 64);
+    poly_scale5(z, zs);
+    if (lane >= s) poly_mul(y, z, zs);
+  }
+  uint32_t R[5], Rs[5], W[5], Ws[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    R[i] = __builtin_amdgcn_readlane(y[i], 63);
+    W[i] = (uint32_t)__shfl((int)y[i], 63 - (int)lane, 64);  // r^(64 - j)
+  }
+  poly_scale5(R, Rs);
+  poly_scale5(W, Ws);
+  const uint32_t M = nc + 1u;
+  const uint32_t T = (M + 63u) >> 6;
+  const uint32_t D = 64u * T - M;
+  uint32_t acc[5] = {0, 0, 0, 0, 0};
+  for (uint32_t t = 0; t < T; ++t) {
+    if (t) poly_mul(acc, R, Rs);
+    const uint32_t p = lane + 64u * t;
+    if (p >= D) {
+      const uint4 v = mac[p - D];
+      uint32_t cl[5];
+      poly_block_limbs(v.x, v.y, v.z, v.w, 1u << 24, cl);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) acc[i] += cl[i];
+    }
+  }
+  poly_mul(acc, W, Ws);
+  // sum over the wave: 32 lanes (limbs stay < 2^32), carry, then the last pair
+#pragma unroll
+  for (int m = 1; m < 32; m <<= 1)
+#pragma unroll
+    for (int i = 0; i < 5; ++i) acc[i] += (uint32_t)__shfl_xor((int)acc[i], m, 64);
+  {
+    uint32_t c;
+    c = acc[0] >> 26; acc[0] &= M26; acc[1] += c;
+    c = acc[1] >> 26; acc[1] &= M26; acc[2] += c;
+    c = acc[2] >> 26; acc[2] &= M26; acc[3] += c;
+    c = acc[3] >> 26; acc[3] &= M26; acc[4] += c;
+    c = acc[4] >> 26; acc[4] &= M26; acc[0] += 5u * c;
+  }
+#pragma unroll
+  for (int i = 0; i < 5; ++i) acc[i] += (uint32_t)__shfl_xor((int)acc[i], 32, 64);
+  uint32_t tag[4];
+  poly_finish(acc, pk[4], pk[5], pk[6], pk[7], tag);
+
+  PP_STAMP(ticket, 4);
+  uint32_t status = WG_PKT_OK;
+  if (open) {  // all 16 bytes compared, no early exit
+    const uint32_t mine = lane < 16u ? ((tag[lane >> 2] >> (8u * (lane & 3u))) & 0xffu) ^ tag_in : 0u;
+    status = __any(mine != 0u) ? WG_PKT_BADTAG : WG_PKT_OK;
+  } else if (lane < 16u) {
+    lds_sync();  // the Horner reads of the MAC image (img_out) before the tag overwrites it
+    ((uint8_t*)img_out)[len + lane] = (uint8_t)(tag[lane >> 2] >> (8u * (lane & 3u)));
+  }
+  lds_sync();
+  // result: system-scope dword stores (write-through to host memory); open writes the
+  // plaintext only when the tag verified
+  const uint32_t n_out = status == WG_PKT_OK ? len + (open ? 0u : 16u) : 0u;
+  {
+    const uint32_t* src = (const uint32_t*)img_out;
+    uint32_t* dst = (uint32_t*)out;
+    const uint32_t nw = (n_out + 3u) >> 2;
+    for (uint32_t k = lane; k < nw; k += 64u) st_sys(dst + k, src[k]);
+  }
+  PP_STAMP(ticket, 5);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every result byte has landed before done
+  PP_STAMP(ticket, 6);
+  if (lane == 0)
+    __hip_atomic_store(done, ((ticket + 1u) << 8) | status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void __launch_bounds__(64) k_pp(PPParams P) {
+  __shared__ uint4 raw[kInSlot / 16 + 4];  // header | payload (+ tag)
+  __shared__ uint4 img_out[kData / 16 + 4];
+  uint4* const img_in = raw + kHdr / 16;
+  const uint32_t w = blockIdx.x;
+  const uint32_t lane = threadIdx.x;
+  uint64_t t = P.next[w];
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t last = t0;
+  uint32_t backoff = 0;
+  for (;;) {
+    const uint32_t i = (uint32_t)(t % kRing);
+    const uint8_t* slot = P.in + (size_t)i * kInSlot;
+    // lane 0: this wave's next ticket published? lane 1: stop flag
+    uint64_t v = 0;
+    if (lane == 0) v = ld_sys64((const uint64_t*)slot);
+    else if (lane == 1) v = ld_sys(&P.ctl->stop);
+    const uint64_t seq = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), 0) << 32) |
+                         __builtin_amdgcn_readlane((uint32_t)v, 0);
+    const uint32_t stop = __builtin_amdgcn_readlane((uint32_t)v, 1);
+    if (seq == t + 1u) {
+      PP_STAMP(t, 0);
+      // header + payload prefix, loaded after seq was seen (the host wrote them before seq):
+      // a system-scope acquire (no stale line of an earlier use of this slot survives in the
+      // CU's caches), then 16-B loads per lane (system-scope dword loads go over PCIe one
+      // request per lane: 7.4 us for these 1536 B, tools/pp_stamps)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#pragma unroll
+      for (uint32_t k = 0; k < kFirstDw / 4; k += 64u)
+        if (k + lane < kFirstDw / 4) raw[k + lane] = ((const uint4*)slot)[k + lane];
+      lds_sync();
+      PP_STAMP(t, 1);
+      Hdr h = *(const Hdr*)raw;
+      h.mode = __builtin_amdgcn_readfirstlane(h.mode);
+      h.len = __builtin_amdgcn_readfirstlane(h.len);
+      if (h.len <= kPPMaxLen && (h.mode == WG_MODE_SEAL || h.mode == WG_MODE_OPEN)) {
+        pp_packet(h, t, slot, P.out + (size_t)i * kOutSlot, P.done + i, img_in, img_out);
+      } else if (lane == 0) {  // refused by the host before publishing; never expected here
+        __hip_atomic_store(P.done + i, ((t + 1u) << 8) | 0xffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      lds_sync();
+      t += P.waves;
+      last = __builtin_amdgcn_s_memrealtime();
+      backoff = 0;
+      continue;
+    }
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    if (stop || now - last > P.idle_ticks || now - t0 > P.life_ticks) break;
+    if (backoff < 2u) ++backoff;  // at most 2 x 256 cycles between polls: latency over PCIe traffic
+    for (uint32_t k = 0; k < backoff; ++k) __builtin_amdgcn_s_sleep(4);  // 4 x 64 cycles per step
+  }
+  if (lane == 0) {
+    P.next[w] = t;
+    __threadfence();
+    if (atomicAdd(P.exited, 1u) == P.waves - 1u)
+      __hip_atomic_store(P.exit_flag, (uint64_t)P.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+}  // namespace wgpp
+
+namespace {
+
+struct PPServer {
+  wg_ctx* c = nullptr;
+  hipStream_t stream = nullptr;
+  uint8_t* host = nullptr;   // pinned, fine-grained: in-slots | out-slots | done | ctl | exit flag
+  uint8_t* dev = nullptr;    // its device alias
+  uint64_t* d_next = nullptr;
+  uint32_t* d_exited = nullptr;
+  std::atomic<uint64_t> tail{0};
+  std::unique_ptr<std::atomic<uint64_t>[]> turn;  // per entry: the ticket allowed to use it next
+  std::mutex launch_mu;
+  std::atomic<uint64_t> running{0};  // gen of the launched kernel (0: none yet)
+  uint64_t gen = 0;                  // guarded by launch_mu
+  uint32_t waves = 16, idle_us = 20000, life_ms = 250;
+  std::atomic<uint64_t> launches{0}, packets{0};
+  int fail_launches = 0;  // test hook (WG_PP_TEST_FAIL_LAUNCHES): refuse this many launches
+
+  uint8_t* in_slot(uint32_t i) { return host + (size_t)i * wgpp::kInSlot; }
+  uint8_t* out_slot(uint32_t i) { return host + (size_t)wgpp::kRing * wgpp::kInSlot + (size_t)i * wgpp::kOutSlot; }
+  size_t done_off() const { return (size_t)wgpp::kRing * (wgpp::kInSlot + wgpp::kOutSlot); }
+  volatile uint64_t* done(uint32_t i) { return (volatile uint64_t*)(host + done_off()) + i; }
+  size_t ctl_off() const { return done_off() + (size_t)wgpp::kRing * 8; }
+  volatile wgpp::Ctl* ctl() { return (volatile wgpp::Ctl*)(host + ctl_off()); }
+  size_t exit_off() const { return ctl_off() + sizeof(wgpp::Ctl); }
+  volatile uint64_t* exit_flag() { return (volatile uint64_t*)(host + exit_off()); }
+  size_t bytes() const { return exit_off() + 64; }
+};
+
+void pp_free(PPServer* S) {
+  if (S->host) (void)hipHostFree(S->host);
+  if (S->d_next) (void)hipFree(S->d_next);
+  if (S->d_exited) (void)hipFree(S->d_exited);
+  if (S->stream) (void)hipStreamDestroy(S->stream);
+}
+
+int pp_get(wg_ctx* c, PPServer** out) {
+  std::lock_guard<std::mutex> lk(c->pp_mu);
+  if (c->pp) {
+    *out = c->pp;
+    return WG_OK;
+  }
+  DeviceGuard g(c->device);
+  PPServer* S = new PPServer();
+  S->c = c;
+  S->turn.reset(new std::atomic<uint64_t>[wgpp::kRing]);
+  for (uint32_t i = 0; i < wgpp::kRing; ++i) S->turn[i].store(i);
+  if (const char* e = getenv("WG_PP_TEST_FAIL_LAUNCHES")) S->fail_launches = atoi(e);
+  bool ok = hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipHostMalloc((void**)&S->host, S->bytes(), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+            hipHostGetDevicePointer((void**)&S->dev, S->host, 0) == hipSuccess &&
+            hipMalloc((void**)&S->d_next, sizeof(uint64_t) * wgpp::kMaxWaves) == hipSuccess &&
+            hipMalloc((void**)&S->d_exited, sizeof(uint32_t)) == hipSuccess;
+  if (ok) {
+    memset(S->host, 0, S->bytes());
+    // wave w starts at ticket w (tickets t = w mod W belong to wave w)
+    uint64_t nx[wgpp::kMaxWaves];
+    for (uint32_t w = 0; w < wgpp::kMaxWaves; ++w) nx[w] = w;
+    ok = hipMemcpy(S->d_next, nx, sizeof nx, hipMemcpyHostToDevice) == hipSuccess;
+  }
+  if (!ok) {
+    pp_free(S);
+    delete S;
+    return fail(WG_ENOMEM, "per-packet server: pinned ring or device state could not be allocated");
+  }
+  c->pp = S;
+  *out = S;
+  return WG_OK;
+}
+
+// (re)launch k_pp unless a launched kernel is still serving (its exit flag != its gen)
+int pp_ensure(PPServer* S) {
+  const uint64_t g = S->running.load(std::memory_order_acquire);
+  if (g && *S->exit_flag() != g) return WG_OK;
+  std::lock_guard<std::mutex> lk(S->launch_mu);
+  const uint64_t g2 = S->running.load(std::memory_order_relaxed);
+  if (g2 && *S->exit_flag() != g2) return WG_OK;
+  DeviceGuard dg(S->c->device);
+  wgpp::PPParams P{};
+  P.in = S->dev;
+  P.out = S->dev + (size_t)wgpp::kRing * wgpp::kInSlot;
+  P.done = (uint64_t*)(S->dev + S->done_off());
+  P.ctl = (const wgpp::Ctl*)(S->dev + S->ctl_off());
+  P.exit_flag = (uint64_t*)(S->dev + S->exit_off());
+  P.next = S->d_next;
+  P.exited = S->d_exited;
+  P.waves = S->waves;
+  P.gen = (uint32_t)(S->gen + 1);
+  P.idle_ticks = (uint64_t)S->idle_us * 100u;
+  P.life_ticks = (uint64_t)S->life_ms * 100000u;
+  if (S->fail_launches > 0) {
+    --S->fail_launches;
+    return fail(WG_EDEVICE, "k_pp launch refused (WG_PP_TEST_FAIL_LAUNCHES test hook)");
+  }
+  HIPTRY(hipMemsetAsync(S->d_exited, 0, sizeof(uint32_t), S->stream));
+  hipLaunchKernelGGL(wgpp::k_pp, dim3(S->waves), dim3(64), 0, S->stream, P);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(WG_EDEVICE, "k_pp launch: %s", hipGetErrorString(e));
+  S->gen += 1;
+  S->running.store(S->gen, std::memory_order_release);
+  S->launches.fetch_add(1, std::memory_order_relaxed);
+  return WG_OK;
+}
+
+void pp_stop(wg_ctx* c) {
+  PPServer* S = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(c->pp_mu);
+    S = c->pp;
+    c->pp = nullptr;
+  }
+  if (!S) return;
+  DeviceGuard g(c->device);
+  S->ctl()->stop = 1;  // every wave sees it at its next poll and exits
+  (void)hipStreamSynchronize(S->stream);
+  pp_free(S);
+  delete S;
+}
+
+// A packet longer than a slot: the host batch path with one descriptor (pageable copy
+// pipeline, device key table).
+int pp_big(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const uint8_t* src, uint32_t len, uint8_t* dst) {
+  wg_pkt d{0, 0, counter, len, key_slot};
+  if (!open) return host_transport(c, false, &d, 1, src, len, dst, (uint64_t)len + 16u, nullptr, len, 0);
+  std::vector<uint8_t> pt(len);
+  uint32_t st = 0;
+  const int rc = host_transport(c, true, &d, 1, src, (uint64_t)len + 16u, pt.data(), len, &st, len, 0);
+  if (rc != WG_OK) return rc;
+  if (st != WG_PKT_OK) return 1;
+  if (len) memcpy(dst, pt.data(), len);
+  return WG_OK;
+}
+
+int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const uint8_t* src, uint32_t len,
+              uint8_t* dst) {
+  if (len > wgpp::kPPMaxLen) return pp_big(c, open, key_slot, counter, src, len, dst);
+  PPServer* S;
+  int rc;
+  if ((rc = pp_get(c, &S)) != WG_OK) return rc;
+  const uint64_t t = S->tail.fetch_add(1, std::memory_order_relaxed);
+  const uint32_t i = (uint32_t)(t % wgpp::kRing);
+  while (S->turn[i].load(std::memory_order_acquire) != t) std::this_thread::yield();  // ring full: wait for t - kRing
+  wgpp::Hdr* h = (wgpp::Hdr*)S->in_slot(i);
+  h->counter = counter;
+  h->mode = open ? WG_MODE_OPEN : WG_MODE_SEAL;
+  h->len = len;
+  {
+    std::lock_guard<std::mutex> lk(c->keys_mu);
+    memcpy(h->key, c->keys_host.data() + (size_t)key_slot * 32, 32);
+  }
+  if (len || open) memcpy(S->in_slot(i) + wgpp::kHdr, src, (size_t)len + (open ? 16u : 0u));
+  __atomic_store_n(&h->seq, t + 1, __ATOMIC_RELEASE);  // publish: after every byte above
+  rc = pp_ensure(S);
+  const uint64_t want = t + 1;
+  uint64_t d = 0;
+  for (uint64_t spin = 1; rc == WG_OK; ++spin) {
+    d = __atomic_load_n((const uint64_t*)S->done(i), __ATOMIC_ACQUIRE);
+    if ((d >> 8) == want) break;
+    if (spin > 4096u) std::this_thread::yield();  // long waits (more callers than cores): let others run
+    if ((spin & 255u) == 0) {
+      rc = pp_ensure(S);  // the kernel may have exited (idle / lifetime) before taking t
+      if (rc == WG_OK && (spin & 0xfffffu) == 0) {
+        const hipError_t e = hipStreamQuery(S->stream);
+        if (e != hipSuccess && e != hipErrorNotReady) rc = fail(WG_EDEVICE, "per-packet server: %s", hipGetErrorString(e));
+      }
+    }
+    __builtin_ia32_pause();
+  }
+  int result = rc;
+  if (rc == WG_OK) {
+    const uint32_t status = (uint32_t)(d & 0xffu);
+    if (status == WG_PKT_OK) {
+      if (open) {
+        if (len) memcpy(dst, S->out_slot(i), len);
+      } else {
+        memcpy(dst, S->out_slot(i), (size_t)len + 16u);
+      }
+    } else {
+      result = status == WG_PKT_BADTAG ? 1 : fail(WG_EDEVICE, "per-packet server refused the packet");
+    }
+    S->packets.fetch_add(1, std::memory_order_relaxed);
+  }
+  memset(h->key, 0, 32);  // no key material left in the ring
+  // on an error the slot stays claimed by this ticket: a late write by the device cannot
+  // reach a later packet's slot
+  if (rc == WG_OK) S->turn[i].store(t + wgpp::kRing, std::memory_order_release);
+  return result;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wg_seal1(wg_ctx* c, uint32_t key_slot, uint64_t counter, const uint8_t* pt, uint32_t len, uint8_t* out) {
+  if (!c || (!pt && len) || !out) return fail(WG_EINVAL, "NULL argument");
+  if (len > WG_MAX_PACKET) return fail(WG_E2BIG, "packet of %u bytes", len);
+  if (key_slot >= c->key_slots) return fail(WG_ERANGE, "key slot %u", key_slot);
+  return pp_submit(c, false, key_slot, counter, pt, len, out);
+}
+
+int wg_open1(wg_ctx* c, uint32_t key_slot, uint64_t counter, const uint8_t* in, uint32_t len, uint8_t* pt) {
+  if (!c || !in || (!pt && len)) return fail(WG_EINVAL, "NULL argument");
+  if (len > WG_MAX_PACKET) return fail(WG_E2BIG, "packet of %u bytes", len);
+  if (key_slot >= c->key_slots) return fail(WG_ERANGE, "key slot %u", key_slot);
+  return pp_submit(c, true, key_slot, counter, in, len, pt);
+}
+
+int wg_batcher_config(wg_ctx* c, uint32_t waves, uint32_t idle_us) {
+  if (!c) return fail(WG_EINVAL, "NULL context");
+  if (waves == 0 || waves > wgpp::kMaxWaves) return fail(WG_EINVAL, "waves must be 1..%u", wgpp::kMaxWaves);
+  PPServer* S;
+  int rc;
+  if ((rc = pp_get(c, &S)) != WG_OK) return rc;
+  std::lock_guard<std::mutex> lk(S->launch_mu);
+  // the wave count fixes which wave owns which ticket: change it only between kernels
+  const uint64_t g = S->running.load();
+  if (g && *S->exit_flag() != g) {
+    S->ctl()->stop = 1;
+    (void)hipStreamSynchronize(S->stream);
+    S->ctl()->stop = 0;
+  }
+  if (waves != S->waves) {
+    // restart the ticket <-> wave map at the next unissued ticket (no call may be in flight)
+    const uint64_t base = S->tail.load();
+    uint64_t nx[wgpp::kMaxWaves];
+    for (uint32_t w = 0; w < wgpp::kMaxWaves; ++w) nx[w] = base + (w + waves - base % waves) % waves;
+    DeviceGuard dg(c->device);
+    HIPTRY(hipMemcpy(S->d_next, nx, sizeof nx, hipMemcpyHostToDevice));
+    S->waves = waves;
+  }
+  S->idle_us = idle_us ? idle_us : 20000;
+  return WG_OK;
+}
+
+int wg_batcher_stats(wg_ctx* c, uint64_t* launches, uint64_t* packets) {
+  if (!c) return fail(WG_EINVAL, "NULL context");
+  uint64_t l = 0, p = 0;
+  {
+    std::lock_guard<std::mutex> lk(c->pp_mu);
+    if (c->pp) {
+      l = c->pp->launches.load();
+      p = c->pp->packets.load();
+    }
+  }
+  if (launches) *launches = l;
+  if (packets) *packets = p;
+  return WG_OK;
+}
+
+}  // extern "C"

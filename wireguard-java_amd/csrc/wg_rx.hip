@@ -121,14 +121,29 @@ void rx_free(wg_ctx* c) {
   c->rx = nullptr;
 }
 
-// zero the replay window of key slots [first, first + n) (a new key = a new session)
+// Orders stream s behind the last replay check (which may sit on another stream): the window
+// state is read and written by the check's kernels, so a reset or a state read must not overtake
+// them. Caller holds c->mu.
+int rx_after_last_check(RxState* r, hipStream_t s) {
+  if (r->ev && r->ev_stream != s && r->ev_stream != (hipStream_t)-1) HIPTRY(hipStreamWaitEvent(s, r->ev, 0));
+  return WG_OK;
+}
+
+// zero the replay window of key slots [first, first + n) (a new key = a new session), in stream
+// order after every replay check queued before it; later checks (any stream) wait for the reset.
+// Caller holds c->mu.
 int rx_reset_slots(wg_ctx* c, uint32_t first, uint32_t n, hipStream_t s) {
   RxState* r = c->rx;
   if (!r || !r->window || !n) return WG_OK;
+  int rc;
+  if ((rc = rx_after_last_check(r, s)) != WG_OK) return rc;
   HIPTRY(hipMemsetAsync((uint64_t*)r->d_top.p + first, 0, (size_t)n * 8, s));
   HIPTRY(hipMemsetAsync((uint64_t*)r->d_newtop.p + first, 0, (size_t)n * 8, s));
   const size_t words = r->window / 64;
   HIPTRY(hipMemsetAsync((uint64_t*)r->d_bits.p + (size_t)first * words, 0, (size_t)n * words * 8, s));
+  if (!r->ev) HIPTRY(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming));
+  HIPTRY(hipEventRecord(r->ev, s));
+  r->ev_stream = s;
   return WG_OK;
 }
 
@@ -541,6 +556,8 @@ int wg_replay_state(wg_ctx* c, uint32_t slot, uint64_t* top, uint64_t* bits, uin
   if (!r || !r->window) return fail(WG_EINVAL, "replay window not enabled");
   if (bits && words != r->window / 64) return fail(WG_EINVAL, "words must be window_bits / 64");
   DeviceGuard g(c->device);
+  int rc;
+  if ((rc = rx_after_last_check(r, c->stream)) != WG_OK) return rc;  // the state after every queued check
   HIPTRY(hipMemcpyAsync(top, (uint64_t*)r->d_top.p + slot, 8, hipMemcpyDeviceToHost, c->stream));
   if (bits)
     HIPTRY(hipMemcpyAsync(bits, (uint64_t*)r->d_bits.p + (size_t)slot * words, (size_t)words * 8,

@@ -40,3 +40,30 @@ def reduce_report(dist, device, timings, payload: float, ok: bool):
     p = torch.tensor([payload, 0.0 if ok else 1.0], dtype=torch.float64, device=device)
     dist.all_reduce(p)
     return t.tolist(), p[0].item(), p[1].item() == 0.0
+
+
+PER_GPU_KEYS = ("elapsed_s", "payload_bytes", "packets", "seal_ms", "open_ms", "kernel_ms")
+
+
+def gather_per_rank(dist, device, row: dict):
+    """Every rank's own figures (PER_GPU_KEYS) gathered to all ranks, in rank order, so the
+    report shows each GPU's rate next to the aggregate (BASELINE configs[3]: per-GPU and
+    aggregate GiB/s; a straggler shows as one low entry). GiB/s per rank = its payload over
+    its own elapsed time."""
+    import torch
+    mine = torch.tensor([float(row[k]) for k in PER_GPU_KEYS], dtype=torch.float64, device=device)
+    world = dist.get_world_size() if dist is not None else 1
+    if world > 1:
+        out = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(out, mine)
+    else:
+        out = [mine]
+    rows = []
+    for r, t in enumerate(out):
+        d = dict(zip(PER_GPU_KEYS, t.tolist()))
+        d["packets"] = int(d["packets"])
+        d["payload_bytes"] = int(d["payload_bytes"])
+        d["rank"] = r
+        d["gib_s"] = d["payload_bytes"] / d["elapsed_s"] / float(1 << 30) if d["elapsed_s"] > 0 else 0.0
+        rows.append(d)
+    return rows

@@ -292,13 +292,13 @@ class Engine:
         rc = L.check(self._lib.wg_open1(self.ctx, slot, counter, src.ctypes.data, n, out.ctypes.data))
         return None if rc == 1 else out[:n].tobytes()
 
-    def batcher_config(self, max_batch: int = 8192, window_us: int = 0) -> None:
-        """wg_batcher_config: packets per batched launch of seal1/open1 and an optional
-        accumulation window in microseconds."""
-        L.check(self._lib.wg_batcher_config(self.ctx, max_batch, window_us))
+    def batcher_config(self, waves: int = 16, idle_us: int = 20000) -> None:
+        """wg_batcher_config: waves of the persistent per-packet server (k_pp) that serves
+        seal1/open1, and how long it stays resident without work (microseconds)."""
+        L.check(self._lib.wg_batcher_config(self.ctx, waves, idle_us))
 
     def batcher_stats(self) -> tuple[int, int]:
-        """(launches, packets) issued by the per-packet batcher so far."""
+        """(server launches, packets served) of the per-packet path so far."""
         a, b = ctypes.c_uint64(), ctypes.c_uint64()
         L.check(self._lib.wg_batcher_stats(self.ctx, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
