@@ -143,6 +143,8 @@ def pmc_valu_insts(mode="serial"):
         return None
     try:
         d = json.load(open(files[-1]))
+        if mode == "step":
+            return d["step"]["counters_mean"]["SQ_INSTS_VALU"] if "step" in d else None
         if mode == "duplex" and "duplex" in d:
             return d["duplex"]["counters_mean"]["SQ_INSTS_VALU"]
         v = [d[k]["counters_mean"]["SQ_INSTS_VALU"] for k in ("seal", "open") if k in d]
@@ -160,6 +162,8 @@ def pmc_traffic(mode="serial"):
         return None
     try:
         d = json.load(open(files[-1]))
+        if mode == "step":
+            return round(d["step_hbm_bytes_per_launch"]) if "step_hbm_bytes_per_launch" in d else None
         if mode == "duplex" and "duplex_hbm_bytes_per_launch" in d:
             return round(d["duplex_hbm_bytes_per_launch"])
         v = [d[k] for k in ("seal_hbm_bytes_per_launch", "open_hbm_bytes_per_launch") if k in d]
@@ -293,7 +297,10 @@ def main():
     # duplex: each step is ONE wg_duplex_batch launch that seals this step's batch and opens
     # the previous step's ciphertext (double-buffered); serial: a seal launch, then an open
     # launch of the same batch
-    ap.add_argument("--mode", default="serial", choices=["serial", "duplex"])
+    # step: ONE wg_duplex_batch(seal, open | WG_F_AFTER_SEAL) per step: the seal launch, then the open
+    # launch of what it sealed (the same two launches as serial; a mixed-length batch is ordered
+    # longest-first once for both); serial: wg_seal_batch, then wg_open_batch
+    ap.add_argument("--mode", default="step", choices=["step", "serial", "duplex"])
     ap.add_argument("--kernel", default="default", help="transport kernel (wg_ctx_set_kernel): default|wave1|tile")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -360,6 +367,13 @@ def main():
     def step():
         if args.mode == "duplex":
             return step_duplex()
+        if args.mode == "step":
+            for i in range(K):
+                a, b = cuts[i], cuts[i + 1]
+                with torch.cuda.stream(side[i]):
+                    eng.duplex(d_desc[a:b], pt, ct, max_len, d_desc[a:b], ct, back, status[a:b], max_len,
+                               uniform=uniform, after_seal=True)
+            return
         for i in range(K):
             a, b = cuts[i], cuts[i + 1]
             with torch.cuda.stream(side[i]):
@@ -444,7 +458,7 @@ def main():
 
     payload = 2.0 * float(lengths.sum())  # sealed + opened bytes per step on this rank
     D = importlib.import_module("wireguard-java_amd.dist")
-    launches = 1 if args.mode == "duplex" else 2  # kernel launches per step
+    launches = 1 if args.mode == "duplex" else 2  # transport kernel launches per step
     # this rank's own figures, gathered before the max-over-ranks reduction (BASELINE configs[3]:
     # per-GPU and aggregate GiB/s)
     per_gpu = D.gather_per_rank(dist if world > 1 else None, dev, {
@@ -466,8 +480,11 @@ def main():
 
     if args.mode == "duplex":
         kname = "k_duplex (seal + open halves)"
+        knames = ["k_duplex"]
     else:
         kname = "k_transport<SEAL|OPEN>" if args.kernel == "default" else args.kernel
+        base = {"default": "k_transport", "transport": "k_transport", "wave1": "k_wave", "tile": "k_tile"}[args.kernel]
+        knames = [base + "<seal>", base + "<open>"]
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -477,6 +494,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ramp_ms": args.ramp_ms,
+            "ramp_steps": ramp_steps,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
             "higher_is_better": True,
             "scaling": "strong" if args.workload == "c3" else "weak",
@@ -488,6 +506,7 @@ def main():
             "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "alg_bytes_per_launch": int(step_alg / launches),
+                         "launches_per_step": launches, "kernel_names": knames,
                          "kernel_ms": round(gpu_step_ms / launches, 5), "seal_ms": round(seal_ms, 5),
                          "open_ms": round(open_ms, 5), "copy_gbs": round(copy_gbs, 1),
                          "frac_of_copy": round(achieved / copy_gbs, 4)},

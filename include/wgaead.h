@@ -143,6 +143,11 @@ int wg_keys_zero(wg_ctx* ctx, uint32_t first_slot, uint32_t n);
  * table given to wg_ctx_set_receivers (k_frame_seal launched after the seal kernel
  * on the same stream). */
 #define WG_F_FRAME 2u
+/* WG_F_RX_FILTER (wg_open_batch only): the open kernel also runs wg_rx_check's WG_RX_FILTER
+ * checks (keepalive, IP version, AllowedIPs of the key slot) on every packet whose tag verified
+ * and writes the refined status itself, in the same launch; the replay window
+ * stays a wg_rx_check call. */
+#define WG_F_RX_FILTER 8u
 /* Device array of receiver_index per key slot (n >= key_slots entries, device memory
  * of this context's device, 4-byte aligned, caller-owned, must outlive the seals that
  * use it); NULL clears it. */
@@ -162,8 +167,13 @@ int wg_open_batch(wg_ctx* ctx, const wg_pkt* desc_dev, uint32_t n, const uint8_t
  * leaves the device idle. The two batches run concurrently: the open batch must not read
  * bytes the seal batch writes in the same call (open the previous call's ciphertext).
  * seal->flags: WG_F_UNIFORM, WG_F_FRAME (as wg_seal_batch); seal->status is ignored.
- * open->flags: WG_F_UNIFORM; open->status is required when open->n > 0.
- * Either n may be 0. */
+ * open->flags: WG_F_UNIFORM, WG_F_AFTER_SEAL; open->status is required when open->n > 0.
+ * Either n may be 0.
+ * WG_F_AFTER_SEAL (open->flags): the open batch DOES read what the seal batch writes: open packet i
+ *   is ordered after seal packet i (same n in both batches; e.g. a loopback or a verify pass over
+ *   what was just sealed). The seal launch and then the open launch run on `stream`; a mixed-length
+ *   batch is ordered longest-first once, for both (its packets have the same lengths). */
+#define WG_F_AFTER_SEAL 4u
 typedef struct wg_batch {
   const wg_pkt* desc; /* device, 16-byte aligned */
   const uint8_t* in;
@@ -227,15 +237,18 @@ int wg_parse_open(wg_ctx* ctx, const uint8_t* wire_dev, uint64_t wire_size, cons
  *   cipher(src, dst): wg_seal1(ctx, send_slot, counter, src, L, dst) with dst of L+16 bytes
  *   decipher(counter, src, dst): wg_open1(ctx, recv_slot, counter, src, L, dst) with src of L+16 bytes
  *   returns WG_OK, or 1 for a bad tag (dst untouched, as NOISE/crypto/ChaCha20Poly1305.java:51-55).
- *   Thread-safe and synchronous per call, but batched underneath (the per-packet
- *   ForkJoinPool fan-out of TransportManager.java:41,79,152-158): the packet is copied
- *   into the open batch (pinned, device-mapped host memory), a library launcher thread
- *   seals/opens everything that accumulated while the previous batch ran, and the
- *   caller returns when its batch completes. Concurrent callers share launches.
- * wg_batcher_config: at most max_batch packets per launch (1..8192, default 8192) and
- *   an optional accumulation window (µs after a batch's first packet; default 0 =
- *   launch as soon as the device is free).
- * wg_batcher_stats: launches and packets the batcher has issued (mean batch size).
+ *   Thread-safe and synchronous per call (the per-packet ForkJoinPool fan-out of
+ *   TransportManager.java:41,79,152-158), served without a kernel launch per packet: the
+ *   packet (with its key, from a host mirror of the key table) goes into a slot of a pinned
+ *   ring, and a persistent device kernel (k_pp: one wave per packet in flight) polls the
+ *   ring over PCIe, seals/opens the packet and writes the result and a completion word back
+ *   into pinned memory, on which the caller spins. The kernel leaves the device after idle_us
+ *   without work (and after at most 250 ms) and the next call relaunches it. Packets longer
+ *   than 4080 bytes (past the reference pipeline's 4-KB buffers) take the host batch path.
+ * wg_batcher_config(ctx, waves, idle_us): waves of that kernel (1..64, default 16; tickets go
+ *   round-robin to waves) and its idle timeout (µs, default 20000; 0 = default). Changing the
+ *   wave count stops a running server first (no call may be in flight).
+ * wg_batcher_stats: server launches and packets served by the per-packet path.
  * wg_seal_host / wg_open_host: a batch in host memory (tun ring in, UDP ring out).
  *   If `in` and `out` are pinned, device-mapped host memory (wg_host_alloc /
  *   wg_host_register) the kernel reads and writes them directly over PCIe
@@ -298,7 +311,7 @@ int wg_rx_check(wg_ctx* ctx, const wg_pkt* desc_dev, uint32_t n, const uint8_t* 
 
 int wg_seal1(wg_ctx* ctx, uint32_t key_slot, uint64_t counter, const uint8_t* pt, uint32_t len, uint8_t* out);
 int wg_open1(wg_ctx* ctx, uint32_t key_slot, uint64_t counter, const uint8_t* in, uint32_t len, uint8_t* pt);
-int wg_batcher_config(wg_ctx* ctx, uint32_t max_batch, uint32_t window_us);
+int wg_batcher_config(wg_ctx* ctx, uint32_t waves, uint32_t idle_us);
 int wg_batcher_stats(wg_ctx* ctx, uint64_t* launches, uint64_t* packets);
 int wg_seal_host(wg_ctx* ctx, const wg_pkt* desc_host, uint32_t n, const uint8_t* in_host, uint64_t in_size,
                  uint8_t* out_host, uint64_t out_size, uint32_t max_len, uint32_t flags);

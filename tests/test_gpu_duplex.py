@@ -127,3 +127,81 @@ def test_duplex_argument_contract(engine):
     with pytest.raises(W.WgError) as e:  # WG_F_FRAME without a receiver table
         engine.duplex(d, buf, buf, 64, d, buf, buf, st, 64, frame=True)
     assert e.value.code == L.WG_EINVAL
+
+
+def _after_seal(engine, n, lengths, nkeys, uniform, forge=()):
+    """wg_duplex_batch(seal, open | WG_F_AFTER_SEAL): seal a batch and, in the same call, open
+    exactly what was sealed. Every ciphertext byte against the oracle, every plaintext byte
+    against the input, statuses all OK."""
+    torch, dev = _dev()
+    W = wg()
+    keys = splitmix_np(0xE0E0 + nkeys, 32 * nkeys)
+    engine.set_keys(0, keys.tobytes())
+    desc, off, total, pt = _batch(0xC0C0 + n, n, lengths, nkeys)
+    d = torch.from_numpy(W.desc_as_int64(desc)).to(dev)
+    dpt = torch.from_numpy(pt).to(dev)
+    dct = torch.zeros(total, dtype=torch.uint8, device=dev)
+    dback = torch.zeros(total, dtype=torch.uint8, device=dev)
+    st = torch.full((n,), 7, dtype=torch.int32, device=dev)
+    m = int(lengths.max())
+    for _ in range(3):  # repeated calls
+        dback.zero_()
+        engine.duplex(d, dpt, dct, m, d, dct, dback, st, m, uniform=uniform, after_seal=True)
+    torch.cuda.synchronize()
+    ref = np.zeros(total, np.uint8)
+    O.seal_batch(desc, pt, ref, keys, threads=16)
+    ct = dct.cpu().numpy()
+    for i in range(n):
+        o, L = int(off[i]), int(lengths[i])
+        assert np.array_equal(ct[o:o + L + 16], ref[o:o + L + 16]), f"ct of packet {i}"
+    back = dback.cpu().numpy()
+    assert (st.cpu().numpy() == 0).all()
+    for i in range(n):
+        o, L = int(off[i]), int(lengths[i])
+        assert np.array_equal(back[o:o + L], pt[o:o + L]), f"plaintext of packet {i}"
+
+
+def test_after_seal_c1_shaped():
+    W = wg()
+    eng = W.Engine(0, key_slots=1)
+    try:
+        _after_seal(eng, 65536, np.full(65536, 1420, np.int64), 1, uniform=True)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("n,L", [(1, 0), (31, 64), (33, 1420), (1000, 577), (4097, 1420)])
+def test_after_seal_ragged_sizes(n, L):
+    W = wg()
+    eng = W.Engine(0, key_slots=8)
+    try:
+        _after_seal(eng, n, np.full(n, L, np.int64), 8, uniform=True)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("n", [3000, 40000])
+def test_after_seal_mixed_lengths(n):
+    """Mixed lengths: 40000 packets take two per slot, so the batch is ordered longest-first once
+    and the open reuses the seal's order."""
+    W = wg()
+    eng = W.Engine(0, key_slots=16)
+    try:
+        lens = (64 + splitmix_np(77, 4 * n).view("<u4") % 3000).astype(np.int64)
+        _after_seal(eng, n, lens, 16, uniform=False)
+    finally:
+        eng.close()
+
+
+def test_after_seal_argument_contract():
+    torch, dev = _dev()
+    W = wg()
+    eng = W.Engine(0, key_slots=1)
+    try:
+        d = torch.zeros((4, 4), dtype=torch.int64, device=dev)
+        b = torch.zeros(64, dtype=torch.uint8, device=dev)
+        st = torch.zeros(3, dtype=torch.int32, device=dev)
+        with pytest.raises(W.WgError):  # unequal sizes
+            eng.duplex(d, b, b, 0, d[:3], b, b, st, 0, uniform=True, after_seal=True)
+    finally:
+        eng.close()

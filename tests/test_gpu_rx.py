@@ -109,6 +109,65 @@ def test_filter_parity_random(engine):
     assert {rx.PKT_OK, rx.PKT_FILTERED, rx.PKT_BADIP, rx.PKT_KEEPALIVE, rx.PKT_BADTAG} <= kinds
 
 
+@pytest.mark.parametrize("uniform", [False, True])
+def test_open_with_fused_filter_matches_open_then_rx_check(engine, uniform):
+    """wg_open_batch(..., WG_F_RX_FILTER): the open kernel writes the receive-side verdict itself.
+    Sealed IP-ish packets (3% forged tags) over 10 key slots and 6 filters; statuses equal
+    oracle open + oracle rx_check, plaintexts equal the inputs."""
+    torch, dev = _dev()
+    W = wg()
+    O = oracle()
+    rng = np.random.default_rng(17)
+    nf = 6
+    filters = {}
+    for f in range(nf):
+        pre = _random_prefixes(rng, int(rng.integers(1, 12)))
+        engine.filter_set(f, pre)
+        o = rx.IPFilter()
+        for a, p in pre:
+            o.insert(a.packed, p)
+        filters[f] = (pre, o)
+    ids = [s % nf for s in range(10)]
+    ids[7] = W._lib.WG_NO_FILTER
+    ids[8] = 4242
+    engine.slot_filters_set(0, ids)
+    keys = splitmix_np(0xF11, 32 * 10)
+    engine.set_keys(0, keys.tobytes())
+    n = 8000
+    slots = rng.integers(0, 10, n)
+    pts = [_packet(rng, filters[ids[int(s)]][0] if ids[int(s)] in filters else []) for s in slots]
+    if uniform:  # equal lengths (the one-packet-per-slot dispatch)
+        pts = [(p + bytes(300))[:300] if len(p) else bytes(300) for p in pts]
+    lens = np.array([len(p) for p in pts], np.int64)
+    S = ((lens + 16 + 15) // 16) * 16
+    off = np.concatenate([[0], np.cumsum(S)[:-1]]).astype(np.uint64)
+    total = int(S.sum())
+    buf = np.zeros(total, np.uint8)
+    for i, p in enumerate(pts):
+        buf[int(off[i]):int(off[i]) + len(p)] = np.frombuffer(p, np.uint8)
+    desc = W.pack_desc(off, off, np.arange(n, dtype=np.uint64), lens, slots)
+    ct = np.zeros(total, np.uint8)
+    O.seal_batch(desc, buf, ct, keys, threads=16)
+    forged = rng.random(n) < 0.03
+    for i in np.nonzero(forged)[0]:
+        ct[int(off[i]) + int(lens[i])] ^= 0x10
+    d = torch.from_numpy(W.desc_as_int64(desc)).to(dev)
+    back = torch.zeros(total, dtype=torch.uint8, device=dev)
+    st = torch.full((n,), 9, dtype=torch.int32, device=dev)
+    engine.open(d, torch.from_numpy(ct).to(dev), back, st, int(lens.max()), uniform=uniform, rx_filter=True)
+    torch.cuda.synchronize()
+    got = st.cpu().numpy().astype(np.int64).tolist()
+    of = {s: (filters[ids[s]][1] if ids[s] in filters else (rx.IPFilter() if ids[s] != W._lib.WG_NO_FILTER else None))
+          for s in range(10)}
+    want = rx.rx_check(slots, np.arange(n), lens.tolist(), pts, forged.astype(np.int64), of, None)
+    assert got == want
+    b = back.cpu().numpy()
+    for i in range(n):
+        o, L = int(off[i]), int(lens[i])
+        exp = np.zeros(L, np.uint8) if forged[i] else buf[o:o + L]
+        assert np.array_equal(b[o:o + L], exp), i
+
+
 def test_reference_filter_known_answers_on_device(engine):
     torch, dev = _dev()
     W = wg()
@@ -230,6 +289,40 @@ def test_replay_then_filter_and_key_reset(engine):
     assert engine.replay_state(0, 128)[0] == 8
     engine.set_keys(0, keys[:32].tobytes())
     assert engine.replay_state(0, 128)[0] == 0
+
+
+def test_rekey_is_ordered_after_replay_checks_on_another_stream():
+    """A replay check queued on a side stream, then wg_keys_set for its slot with no
+    synchronisation in between: the window reset must land after the queued check,
+    so the new session's counters from 0 are accepted, not rejected as too old."""
+    torch, dev = _dev()
+    W = wg()
+    eng = W.Engine(0, key_slots=4)
+    try:
+        eng.replay_enable(256)
+        eng.set_keys(0, splitmix_np(21, 32 * 4).tobytes())
+        n = 60000
+        desc = W.pack_desc(np.zeros(n, np.uint64), np.zeros(n, np.uint64), np.arange(1_000_000, 1_000_000 + n),
+                           np.zeros(n, np.int64), np.zeros(n, np.int64))
+        d = torch.from_numpy(W.desc_as_int64(desc)).to(dev)
+        pt = torch.zeros(64, dtype=torch.uint8, device=dev)
+        side = torch.cuda.Stream(device=dev)
+        for _ in range(3):
+            st = torch.zeros(n, dtype=torch.int32, device=dev)
+            torch.cuda.synchronize()
+            with torch.cuda.stream(side):
+                eng.rx_check(d, pt, st, W._lib.WG_RX_REPLAY)  # old session: top -> 1,060,000
+            eng.set_keys(0, splitmix_np(22, 32).tobytes())      # new session, no sync before it
+            fresh = W.pack_desc(np.zeros(4, np.uint64), np.zeros(4, np.uint64), np.arange(4), np.zeros(4, np.int64),
+                                np.zeros(4, np.int64))
+            st2 = torch.zeros(4, dtype=torch.int32, device=dev)
+            eng.rx_check(torch.from_numpy(W.desc_as_int64(fresh)).to(dev), pt, st2, W._lib.WG_RX_REPLAY)
+            torch.cuda.synchronize()
+            assert (st.cpu().numpy() == rx.PKT_OK).all()  # the old batch: all fresh counters
+            assert st2.cpu().tolist() == [rx.PKT_OK] * 4  # counters 0..3 of the new session accepted
+            assert eng.replay_state(0, 256)[0] == 4
+    finally:
+        eng.close()
 
 
 def test_rx_argument_contract(engine):

@@ -1,7 +1,10 @@
-"""Timing of wg_rx_check on a C1-shaped opened batch (65536 x 1420 B IPv4 plaintexts, one
-key slot with a 3-prefix AllowedIPs filter): filter only, replay only, both. HIP events on
-the launch stream around each of 200 calls; the replay window is re-enabled (emptied,
-untimed) before each call so every call sees fresh counters."""
+"""Timing of the receive side on a C1-shaped batch (65536 x 1420 B IPv4 plaintexts, one key slot
+with a 3-prefix AllowedIPs filter), after a 150-ms clock ramp:
+  open, open with the fused filter (wg_open_batch WG_F_RX_FILTER), open then wg_rx_check(FILTER);
+  wg_rx_check alone: filter, replay, both; replay over 1024 key slots.
+HIP events on the launch stream around each of 200 calls (open variants: 200 calls each,
+alternating between the variants); the replay window is re-enabled (emptied, untimed) before each
+replay call so every call sees fresh counters."""
 import json
 import os
 import sys
@@ -31,6 +34,35 @@ def main():
     st0 = torch.zeros(n, dtype=torch.int32, device=dev)
     st = st0.clone()
     out = {"n": n}
+    eng.set_keys(0, bytes(range(32)))
+    ct = torch.zeros_like(dpt)
+    back = torch.zeros_like(dpt)
+    eng.seal(d, dpt, ct, L, uniform=True)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    import time
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.15:  # clock ramp
+        eng.open(d, ct, back, st, L, uniform=True, rx_filter=True)
+        eng.rx_check(d, back, st, 1)
+        torch.cuda.synchronize()
+    variants = {
+        "open": lambda: eng.open(d, ct, back, st, L, uniform=True),
+        "open_fused_filter": lambda: eng.open(d, ct, back, st, L, uniform=True, rx_filter=True),
+        "open_then_rx_filter": lambda: (eng.open(d, ct, back, st, L, uniform=True), eng.rx_check(d, back, st, 1)),
+    }
+    tot = {k: 0.0 for k in variants}
+    for _ in range(200):
+        for k, f in variants.items():
+            a.record()
+            f()
+            b.record()
+            torch.cuda.synchronize()
+            tot[k] += a.elapsed_time(b)
+    for k in variants:
+        out[k + "_us"] = round(tot[k] / 200 * 1e3, 2)
+    variants["open_fused_filter"]()
+    torch.cuda.synchronize()
+    out["open_fused_filter_status_hist"] = np.bincount(st.cpu().numpy(), minlength=7).tolist()
     for name, flags in (("filter", 1), ("replay", 2), ("filter+replay", 3)):
         if flags & 2:
             eng.replay_enable(8192)

@@ -1,52 +1,68 @@
 #!/bin/bash
 # One measurement round on the GPU box (run through gpurun from the repo root):
-#   parity tests, smoke(), bench lines (C1 with cpu_baseline, C2, C3), the
-#   rocprofv3 --kernel-trace --stats summary of the C1 bench command, and one PMC
-#   pass per counter (FETCH_SIZE, WRITE_SIZE, VALU/wave counters) over the same command.
-# Usage: bash tools/gpu_round.sh r01 [quick]
-set -eo pipefail
-R=${1:-r01}
+#   parity tests, smoke(), bench lines (C1 step with cpu_baseline, C1 serial, C2, C3, C4 host),
+#   the UDP host pipeline, receive-side and per-packet timings, rocprofv3 kernel traces of the
+#   C1 and C2 bench commands (tools/prof_window.py keeps the timed region only) and one PMC pass
+#   per counter group for C1 and C2 (each pass its own run, as the MI355X guide prescribes).
+# Usage: bash tools/gpu_round.sh r03 [quick]
+set -o pipefail
+R=${1:-r03}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$ROOT/gpurun_out/$R
 mkdir -p $O $O/pmc
 cd $ROOT
-echo "[round] tests"; timeout -k 10 600 python -m pytest tests -x -q -m gpu > $O/gpu_tests.log 2>&1
+step() { echo "[round] $1"; }
+die() { echo "[round] FAILED: $1 (rc $2)"; exit $2; }
+step tests
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 || die tests $?
 tail -1 $O/gpu_tests.log
-echo "[round] smoke"; timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+step smoke
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || die smoke $?
 tail -1 $O/smoke.log
-echo "[round] bench c1"; timeout -k 10 400 python bench.py > $O/bench_c1.json 2> $O/bench.err
+step "bench c1 (step)"
+timeout -k 10 400 python bench.py > $O/bench_c1.json 2> $O/bench.err || die bench_c1 $?
 cat $O/bench_c1.json
-echo "[round] bench c2"; timeout -k 10 300 python bench.py --workload c2 > $O/bench_c2.json 2>> $O/bench.err
+step "bench c1 (serial)"
+timeout -k 10 300 python bench.py --mode serial --no-cpu-baseline > $O/bench_c1_serial.json 2>> $O/bench.err || die bench_c1_serial $?
+step "bench c2"
+timeout -k 10 300 python bench.py --workload c2 > $O/bench_c2.json 2>> $O/bench.err || die bench_c2 $?
 cat $O/bench_c2.json
 if [ "$2" != "quick" ]; then
-  echo "[round] bench c3"; timeout -k 10 400 python bench.py --workload c3 --no-cpu-baseline --steps 5 --warmup 1 > $O/bench_c3.json 2>> $O/bench.err
+  step "bench c3"
+  timeout -k 10 400 python bench.py --workload c3 --no-cpu-baseline --steps 5 --warmup 1 > $O/bench_c3.json 2>> $O/bench.err || die bench_c3 $?
   cat $O/bench_c3.json
+  step "host path c4"
+  timeout -k 10 300 python bench.py --workload c4 --steps 5 --warmup 1 > $O/bench_c4_pinned.json 2>> $O/bench.err || die c4 $?
+  WG_HOST_PATH=copy timeout -k 10 300 python bench.py --workload c4 --steps 5 --warmup 1 > $O/bench_c4_pinned_copy.json 2>> $O/bench.err || die c4copy $?
+  timeout -k 10 300 python bench.py --workload c4 --host-mem pageable --steps 3 --warmup 1 > $O/bench_c4_pageable.json 2>> $O/bench.err || die c4pageable $?
+  cat $O/bench_c4_*.json
+  step "host-to-host pipeline (UDP loopback)"
+  for k in 1 8; do
+    timeout -k 10 200 ./tools/host_pipeline --backend gpu --packets 65536 --reps 5 --udp-streams $k --tun >> $O/host_pipeline_gpu.jsonl || die pipeline $?
+  done
+  timeout -k 10 300 ./tools/host_pipeline --backend cpu --oracle oracle/liboracle.so --threads 16 --packets 65536 --reps 3 --udp-streams 8 --tun >> $O/host_pipeline_cpu.jsonl || die pipeline_cpu $?
 fi
-echo "[round] host path c4"
-timeout -k 10 300 python bench.py --workload c4 --steps 5 --warmup 1 > $O/bench_c4_pinned.json 2>> $O/bench.err
-cat $O/bench_c4_pinned.json
-WG_HOST_PATH=copy timeout -k 10 300 python bench.py --workload c4 --steps 5 --warmup 1 > $O/bench_c4_pinned_copy.json 2>> $O/bench.err
-cat $O/bench_c4_pinned_copy.json
-timeout -k 10 300 python bench.py --workload c4 --host-mem pageable --steps 3 --warmup 1 > $O/bench_c4_pageable.json 2>> $O/bench.err
-cat $O/bench_c4_pageable.json
-echo "[round] host-to-host pipeline (UDP loopback)"
-for k in 1 8; do
-  timeout -k 10 200 ./tools/host_pipeline --backend gpu --packets 65536 --reps 5 --udp-streams $k --tun >> $O/host_pipeline_gpu.jsonl
-done
-timeout -k 10 300 ./tools/host_pipeline --backend cpu --oracle oracle/liboracle.so --threads 16 --packets 65536 --reps 3 --udp-streams 8 --tun >> $O/host_pipeline_cpu.jsonl
-cat $O/host_pipeline_gpu.jsonl $O/host_pipeline_cpu.jsonl
-echo "[round] receive-side checks"; timeout -k 10 120 python tools/bench_rx.py > $O/rx_timing.json; cat $O/rx_timing.json
-echo "[round] per-packet batcher"
-for t in 1 16 64; do timeout -k 10 120 ./tools/batcher_bench $t $((t == 1 ? 2000 : 160000 / t)) 1420 >> $O/batcher.jsonl; done
-timeout -k 10 120 ./tools/batcher_bench 16 10000 0 >> $O/batcher.jsonl
+step "receive side"
+timeout -k 10 180 python tools/bench_rx.py > $O/rx_timing.json || die rx $?
+cat $O/rx_timing.json
+step "per-packet server"
+for t in 1 16 64; do timeout -k 10 120 ./tools/batcher_bench $t $((t == 1 ? 4000 : 160000 / t)) 1420 >> $O/batcher.jsonl || die batcher $?; done
+timeout -k 10 120 ./tools/batcher_bench 16 10000 0 >> $O/batcher.jsonl || die batcher_mixed $?
 cat $O/batcher.jsonl
+timeout -k 10 120 ./tools/pp_stamps 1420 > $O/pp_stamps.json || die pp_stamps $?
 cd /tmp && export TMPDIR=/tmp
-echo "[round] rocprofv3 stats"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $ROOT/bench.py --no-cpu-baseline > $O/prof_bench.json 2> $O/prof.log
-i=0
-for grp in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do
-  i=$((i+1))
-  echo "[round] pmc $grp"
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d $O/pmc/p$i -o run --output-format csv -- python3 $ROOT/bench.py --no-cpu-baseline --steps 5 --warmup 1 > $O/pmc/p$i.log 2>&1
+for w in c1 c2; do
+  step "rocprofv3 kernel trace $w"
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_$w -o run --output-format csv -- python3 $ROOT/bench.py --workload $w --no-cpu-baseline > $O/prof_bench_$w.json 2> $O/prof_$w.log || die prof_$w $?
+  python3 $ROOT/tools/prof_window.py trace $(find $O/prof_$w -name "run_kernel_trace.csv" | head -1) $O/prof_bench_$w.json --out $O/window_$w.json > /dev/null || die window_$w $?
+  i=0
+  for grp in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE"; do
+    i=$((i+1))
+    step "pmc $w $grp"
+    timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d $O/pmc/${w}_p$i -o run --output-format csv -- python3 $ROOT/bench.py --workload $w --no-cpu-baseline --steps 20 --warmup 2 > $O/pmc/${w}_p$i.json 2> $O/pmc/${w}_p$i.log || die pmc_$w_$i $?
+  done
+  args=""
+  for j in 1 2 3 4; do args="$args $(find $O/pmc/${w}_p$j -name '*counter_collection.csv' | head -1) $O/pmc/${w}_p$j.json"; done
+  python3 $ROOT/tools/prof_window.py pmc $args --out $O/pmc_$w.json > /dev/null || die pmc_window_$w $?
 done
-echo "[round] done"
+step done

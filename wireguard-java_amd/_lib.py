@@ -38,6 +38,8 @@ WG_KEY_SIZE = 32
 WG_MAX_PACKET = 65535
 WG_F_UNIFORM = 1
 WG_F_FRAME = 2
+WG_F_AFTER_SEAL = 4
+WG_F_RX_FILTER = 8
 WG_MODE_SEAL, WG_MODE_OPEN, WG_MODE_CIPHER, WG_MODE_MAC = 0, 1, 2, 3
 
 _ERRNAMES = {WG_EINVAL: "EINVAL", WG_ENOMEM: "ENOMEM", WG_ERANGE: "ERANGE", WG_E2BIG: "E2BIG",

@@ -77,6 +77,7 @@ enum Kern { KERN_TRANSPORT = 0, KERN_WAVE1 = 1, KERN_TILE = 2 };
 
 struct PPServer;  // wg_pp.hip
 void pp_stop(wg_ctx* c);
+int rx_tables(wg_ctx* c, const wgt::RxTables** out);  // wg_rx.hip
 struct RxState;  // wg_rx.hip
 
 }  // namespace
@@ -96,6 +97,7 @@ struct wg_ctx {
   // plan workspace: k_tile block scan, k_transport longest-first order
   DevBuf plan_nb, plan_prefix, plan_tiles, plan_ntiles, plan_tmp, lpt_hist, lpt_order;
   DevBuf lpt_hist2, lpt_order2;  // the open half of a wg_duplex_batch
+
   int kern = KERN_TRANSPORT;
   // host-API staging
   DevBuf h_desc, h_in, h_out, h_aad, h_status, h_keys;
@@ -284,7 +286,8 @@ template <int MODE>
 int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, uint64_t in_size, uint8_t* out,
                    uint64_t out_size, uint32_t* status, uint32_t max_len, uint32_t flags, hipStream_t s,
                    uint64_t cap_slots, DevBuf& lpt_hist, DevBuf& lpt_order, wgt::TransportParams* Pout,
-                   uint32_t* grid_out, bool* ordered_out) {
+                   uint32_t* grid_out, bool* ordered_out, const wgt::RxTables* rx = nullptr,
+                   bool private_ws = false, bool reuse_order = false) {
   bool ordered = false;
   wgt::TransportParams P{};
   P.desc = desc;
@@ -297,6 +300,7 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   P.out_size = out_size;
   P.keys = c->keys;
   P.status = status;
+  P.rx = MODE == WG_MODE_OPEN ? rx : nullptr;
 #ifdef WG_DIAG
   P.stamps = g_stamps;
 #endif
@@ -322,18 +326,22 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   const uint32_t max_rounds = (host_pkt_blocks<WG_MODE_SEAL>(max_len) + 7u) / 8u;
   P.prio_step = (flags & WG_F_UNIFORM) ? 0u : std::max<uint32_t>(1u, (uint32_t)((per_slot * max_rounds + 3u) / 4u));
   if (!(flags & WG_F_UNIFORM) && per_slot > 1) {  // longest-first order (LPT) for the snake
-    int rc;
-    const uint32_t lgrid = std::max<uint32_t>(1u, std::min<uint32_t>(wgt::LPT_MAX_BLOCKS, (n + 1023u) / 1024u));
-    if ((rc = lpt_hist.ensure(sizeof(uint32_t) * wgt::LPT_MAX_BLOCKS * wgt::LPT_BINS)) != WG_OK) return rc;
-    if ((rc = lpt_order.ensure(sizeof(uint32_t) * (size_t)n)) != WG_OK) return rc;
-    if ((rc = ws_acquire(c, s)) != WG_OK) return rc;
-    uint32_t* bh = (uint32_t*)lpt_hist.p;
-    hipLaunchKernelGGL((wgt::k_lpt_hist<MODE>), dim3(lgrid), dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len, bh);
-    hipLaunchKernelGGL((wgt::k_lpt_scatter<MODE>), dim3(lgrid), dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len,
-                       (const uint32_t*)bh, (uint32_t*)lpt_order.p);
-    HIPTRY(hipGetLastError());
+    // reuse_order: the order already in lpt_order (the seal of the same packets, WG_F_AFTER_SEAL);
+    // private_ws: buffers owned by the caller's stream (no shared-workspace ordering)
+    if (!reuse_order) {
+      int rc;
+      const uint32_t lgrid = std::max<uint32_t>(1u, std::min<uint32_t>(wgt::LPT_MAX_BLOCKS, (n + 1023u) / 1024u));
+      if ((rc = lpt_hist.ensure(sizeof(uint32_t) * wgt::LPT_MAX_BLOCKS * wgt::LPT_BINS)) != WG_OK) return rc;
+      if ((rc = lpt_order.ensure(sizeof(uint32_t) * (size_t)n)) != WG_OK) return rc;
+      if (!private_ws && (rc = ws_acquire(c, s)) != WG_OK) return rc;
+      uint32_t* bh = (uint32_t*)lpt_hist.p;
+      hipLaunchKernelGGL((wgt::k_lpt_hist<MODE>), dim3(lgrid), dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len, bh);
+      hipLaunchKernelGGL((wgt::k_lpt_scatter<MODE>), dim3(lgrid), dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len,
+                         (const uint32_t*)bh, (uint32_t*)lpt_order.p);
+      HIPTRY(hipGetLastError());
+    }
     P.order = (const uint32_t*)lpt_order.p;
-    ordered = true;
+    ordered = !private_ws;
   }
   *Pout = P;
   *grid_out = grid;
@@ -346,7 +354,9 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
 // the device first (k_lpt_*), so the slots' snake over the order balances their rounds.
 template <int MODE>
 int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, uint64_t in_size, uint8_t* out,
-                     uint64_t out_size, uint32_t* status, uint32_t max_len, uint32_t flags, hipStream_t s) {
+                     uint64_t out_size, uint32_t* status, uint32_t max_len, uint32_t flags, hipStream_t s,
+                     const wgt::RxTables* rx = nullptr, DevBuf* own_hist = nullptr, DevBuf* own_order = nullptr,
+                     bool reuse_order = false) {
   if (n == 0) return WG_OK;
   if (!desc || (((uintptr_t)desc) & 15u)) return fail(WG_EINVAL, "descriptor array must be non-NULL and 16-byte aligned");
   if (!in || !out) return fail(WG_EINVAL, "NULL buffer");
@@ -381,8 +391,11 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
   uint32_t grid = 0;
   bool ordered = false;
   const uint64_t cap_slots = 8ull * std::max<uint32_t>(c->resident_waves[MODE == WG_MODE_OPEN], wgt::TW);
+  if (rx && c->kern != KERN_TRANSPORT) return fail(WG_EINVAL, "WG_F_RX_FILTER needs the transport kernel");
+  const bool own = own_hist && own_order;  // the caller holds the plan workspace (launch_after_seal)
   int rc = plan_transport<MODE>(c, desc, n, in, in_size, out, out_size, status, max_len, flags, s, cap_slots,
-                                c->lpt_hist, c->lpt_order, &P, &grid, &ordered);
+                                own ? *own_hist : c->lpt_hist, own ? *own_order : c->lpt_order, &P, &grid, &ordered,
+                                rx, own, reuse_order);
   if (rc != WG_OK) return rc;
   hipEvent_t ev;
   record_start(c, s, &ev);
@@ -394,6 +407,25 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
 }
 
 hipStream_t pick_stream(wg_ctx*, void* stream) { return (hipStream_t)stream; }
+
+// wg_duplex_batch(seal, open | WG_F_AFTER_SEAL): the seal launch, then the open launch of what it
+// wrote, on `s`. A mixed-length batch is ordered longest-first once: the open's packets have the
+// seal's lengths, so it reuses the seal's order (one k_lpt_* pair per step instead of two). The
+// plan workspace is held from the seal's order to the open. Caller holds c->mu.
+int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStream_t s) {
+  const bool same_plan = sb->max_len == ob->max_len && (sb->flags & WG_F_UNIFORM) == (ob->flags & WG_F_UNIFORM) &&
+                         c->resident_waves[0] == c->resident_waves[1];
+  int rc;
+  if ((rc = ws_acquire(c, s)) != WG_OK) return rc;
+  rc = launch_transport<WG_MODE_SEAL>(c, sb->desc, sb->n, sb->in, sb->in_size, sb->out, sb->out_size, nullptr,
+                                      sb->max_len, sb->flags, s, nullptr, &c->lpt_hist, &c->lpt_order);
+  if (rc == WG_OK)
+    rc = launch_transport<WG_MODE_OPEN>(c, ob->desc, ob->n, ob->in, ob->in_size, ob->out, ob->out_size, ob->status,
+                                        ob->max_len, ob->flags & ~WG_F_AFTER_SEAL, s, nullptr, &c->lpt_hist,
+                                        &c->lpt_order, same_plan);
+  const int rr = ws_release(c, s);
+  return rc != WG_OK ? rc : rr;
+}
 
 }  // namespace
 
@@ -480,7 +512,8 @@ int wg_ctx_destroy(wg_ctx* c) {
     (void)hipEventDestroy(e.second);
   }
   for (DevBuf* b : {&c->plan_nb, &c->plan_prefix, &c->plan_tiles, &c->plan_ntiles, &c->plan_tmp, &c->lpt_hist,
-                    &c->lpt_order, &c->lpt_hist2, &c->lpt_order2, &c->h_desc, &c->h_in, &c->h_out, &c->h_aad, &c->h_status, &c->h_keys})
+                    &c->lpt_order, &c->lpt_hist2, &c->lpt_order2, &c->h_desc, &c->h_in, &c->h_out, &c->h_aad, &c->h_status,
+                    &c->h_keys})
     b->release();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -575,28 +608,40 @@ int wg_ctx_set_receivers(wg_ctx* c, const uint32_t* receivers, uint32_t n) {
 int wg_open_batch(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, uint64_t in_size, uint8_t* out,
                   uint64_t out_size, uint32_t* status, uint32_t max_len, uint32_t flags, void* stream) {
   if (!c) return fail(WG_EINVAL, "NULL context");
-  if (flags & ~WG_F_UNIFORM) return fail(WG_EINVAL, "open takes only WG_F_UNIFORM (flags 0x%x)", flags);
+  if (flags & ~(WG_F_UNIFORM | WG_F_RX_FILTER))
+    return fail(WG_EINVAL, "open takes only WG_F_UNIFORM | WG_F_RX_FILTER (flags 0x%x)", flags);
   if (n && !status) return fail(WG_EINVAL, "open needs a status array");
   DeviceGuard g(c->device);
   std::lock_guard<std::mutex> lk(c->mu);
-  return launch_transport<WG_MODE_OPEN>(c, desc, n, in, in_size, out, out_size, status, max_len, flags,
-                                       pick_stream(c, stream));
+  const wgt::RxTables* rx = nullptr;
+  if (flags & WG_F_RX_FILTER) {
+    int rc;
+    if ((rc = rx_tables(c, &rx)) != WG_OK) return rc;
+  }
+  return launch_transport<WG_MODE_OPEN>(c, desc, n, in, in_size, out, out_size, status, max_len,
+                                       flags & ~WG_F_RX_FILTER, pick_stream(c, stream), rx);
 }
 
 // Seal one batch and open another in one k_duplex launch (wg_duplex_batch).
 int wg_duplex_batch(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, void* stream) {
   if (!c || !sb || !ob) return fail(WG_EINVAL, "NULL argument");
   if (sb->flags & ~kFlagsKnown) return fail(WG_EINVAL, "unknown seal flag bits 0x%x", sb->flags & ~kFlagsKnown);
-  if (ob->flags & ~WG_F_UNIFORM) return fail(WG_EINVAL, "open takes only WG_F_UNIFORM (flags 0x%x)", ob->flags);
+  if (ob->flags & ~(WG_F_UNIFORM | WG_F_AFTER_SEAL))
+    return fail(WG_EINVAL, "open takes only WG_F_UNIFORM | WG_F_AFTER_SEAL (flags 0x%x)", ob->flags);
   if (ob->n && !ob->status) return fail(WG_EINVAL, "open needs a status array");
+  const bool after = (ob->flags & WG_F_AFTER_SEAL) != 0;
+  if (after && sb->n != ob->n) return fail(WG_EINVAL, "WG_F_AFTER_SEAL needs equal batch sizes (%u, %u)", sb->n, ob->n);
   DeviceGuard g(c->device);
   hipStream_t s = pick_stream(c, stream);
   {
     std::lock_guard<std::mutex> lk(c->mu);
     if ((sb->flags & WG_F_FRAME) && !c->receivers)
       return fail(WG_EINVAL, "WG_F_FRAME without a receiver table (wg_ctx_set_receivers)");
-    const bool fused = c->kern == KERN_TRANSPORT && sb->n && ob->n;
-    if (fused) {
+    const bool fused = !after && c->kern == KERN_TRANSPORT && sb->n && ob->n;
+    if (after && c->kern == KERN_TRANSPORT && sb->n) {
+      int rc = launch_after_seal(c, sb, ob, s);
+      if (rc != WG_OK) return rc;
+    } else if (fused) {
       for (const wg_batch* b : {sb, ob}) {
         if (!b->desc || (((uintptr_t)b->desc) & 15u))
           return fail(WG_EINVAL, "descriptor array must be non-NULL and 16-byte aligned");
@@ -626,7 +671,7 @@ int wg_duplex_batch(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, void* str
                                               sb->max_len, sb->flags, s);
       if (rc != WG_OK) return rc;
       rc = launch_transport<WG_MODE_OPEN>(c, ob->desc, ob->n, ob->in, ob->in_size, ob->out, ob->out_size, ob->status,
-                                          ob->max_len, ob->flags, s);
+                                          ob->max_len, ob->flags & ~WG_F_AFTER_SEAL, s);
       if (rc != WG_OK) return rc;
     }
     if (!(sb->flags & WG_F_FRAME) || sb->n == 0) return WG_OK;

@@ -61,6 +61,8 @@ struct RxState {
   DevBuf d_flag;            // k_rp_order's flag (0 between calls)
   hipEvent_t ev = nullptr;  // last use of the replay scratch, and its stream (stream-ordered reuse)
   hipStream_t ev_stream = (hipStream_t)-1;
+  DevBuf d_tables;          // wgt::RxTables for the fused open (WG_F_RX_FILTER)
+  bool tables_valid = false;
 };
 
 // ---- host: IPFilter.insert as a binary trie, then stride-8 tables -------------------------
@@ -114,11 +116,31 @@ void rx_free(wg_ctx* c) {
   if (!c->rx) return;
   RxState* r = c->rx;
   for (DevBuf* b : {&r->d_entries, &r->d_hdr, &r->d_slot_filter, &r->d_top, &r->d_bits, &r->d_newtop, &r->d_tab,
-                    &r->d_pos, &r->d_flag})
+                    &r->d_pos, &r->d_flag, &r->d_tables})
     b->release();
   if (r->ev) (void)hipEventDestroy(r->ev);
   delete r;
   c->rx = nullptr;
+}
+
+// The RxTables struct the fused open reads (wg_open_batch with WG_F_RX_FILTER), rebuilt after
+// every filter / slot-map change. Caller holds c->mu.
+int rx_tables(wg_ctx* c, const wgt::RxTables** out) {
+  RxState* r;
+  rx_get(c, &r);
+  int rc;
+  if ((rc = r->d_tables.ensure(sizeof(wgt::RxTables))) != WG_OK) return rc;
+  if (!r->tables_valid) {
+    const wgt::RxTables T{r->slot_filter_init ? (const uint32_t*)r->d_slot_filter.p : nullptr,
+                          (const uint32_t*)r->d_hdr.p, (const uint32_t*)r->d_entries.p,
+                          (uint32_t)r->filt_roots.size(), c->key_slots};
+    DeviceGuard g(c->device);
+    HIPTRY(hipMemcpyAsync(r->d_tables.p, &T, sizeof T, hipMemcpyHostToDevice, c->stream));
+    HIPTRY(hipStreamSynchronize(c->stream));
+    r->tables_valid = true;
+  }
+  *out = (const wgt::RxTables*)r->d_tables.p;
+  return WG_OK;
 }
 
 // Orders stream s behind the last replay check (which may sit on another stream): the window
@@ -397,47 +419,18 @@ __global__ void __launch_bounds__(256) k_rp_mark(RxParams P) {
   if (i == 0) *P.unsorted = 0u;  // k_rp_decide was its last reader: 0 again for the next batch
 }
 
-// keepalive / IP version / AllowedIPs, one thread per packet
+// keepalive / IP version / AllowedIPs, one thread per packet (wgt::rx_verdict, shared with the
+// fused open of wg_open_batch(..., WG_F_RX_FILTER))
 __global__ void __launch_bounds__(256) k_rx_filter(RxParams P) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   if (i >= P.n || P.status[i] != WG_PKT_OK) return;
   const wg_pkt d = P.desc[i];
-  if (d.len == 0) {
-    P.status[i] = WG_PKT_KEEPALIVE;
-    return;
-  }
-  if (d.out_off >= P.pt_size || P.pt_size - d.out_off < d.len) {
+  if (d.len && (d.out_off >= P.pt_size || P.pt_size - d.out_off < d.len)) {
     P.status[i] = WG_PKT_BADIP;  // not readable here (open would have rejected it already)
     return;
   }
-  const uint8_t* p = P.pt + d.out_off;
-  const uint32_t ver = p[0] >> 4;
-  uint32_t nbytes, at;
-  if (ver == 4) {
-    nbytes = 4;
-    at = 16;
-  } else if (ver == 6) {
-    nbytes = 16;
-    at = 24;
-  } else {
-    P.status[i] = WG_PKT_BADIP;  // destinationIPOf throws IllegalArgumentException
-    return;
-  }
-  if (d.len < at + nbytes) {
-    P.status[i] = WG_PKT_BADIP;  // slice out of bounds
-    return;
-  }
-  if (!P.slot_filter || d.key_slot >= P.key_slots) return;
-  const uint32_t f = P.slot_filter[d.key_slot];
-  if (f == kRxNoFilter) return;
-  uint32_t node = f < P.nfilters ? P.hdr[2 * f + (ver == 6 ? 1 : 0)] : 0u;  // never set: empty filter
-  bool found = false;
-  for (uint32_t L = 0; L < nbytes && node; ++L) {
-    const uint32_t e = P.entries[(size_t)node * 256 + p[at + L]];
-    found |= (e >> 31) != 0;
-    node = e & 0x7FFFFFFFu;
-  }
-  if (!found) P.status[i] = WG_PKT_FILTERED;
+  const wgt::RxTables T{P.slot_filter, P.hdr, P.entries, P.nfilters, P.key_slots};
+  P.status[i] = wgt::rx_verdict(T, P.pt + d.out_off, d.len, d.key_slot);
 }
 
 }  // namespace wgrx
@@ -493,6 +486,7 @@ int wg_filter_set(wg_ctx* c, uint32_t filter_id, const wg_prefix* prefixes, uint
   HIPTRY(hipMemcpyAsync(r->d_entries.p, all.data(), all.size() * 4, hipMemcpyHostToDevice, c->stream));
   HIPTRY(hipMemcpyAsync(r->d_hdr.p, hdr.data(), hdr.size() * 4, hipMemcpyHostToDevice, c->stream));
   HIPTRY(hipStreamSynchronize(c->stream));
+  r->tables_valid = false;  // the tables may have moved
   return WG_OK;
 }
 
@@ -513,6 +507,7 @@ int wg_slot_filters_set(wg_ctx* c, uint32_t first_slot, uint32_t n, const uint32
   if (n) HIPTRY(hipMemcpyAsync((uint32_t*)r->d_slot_filter.p + first_slot, filter_ids, (size_t)n * 4,
                                hipMemcpyHostToDevice, c->stream));
   HIPTRY(hipStreamSynchronize(c->stream));
+  r->tables_valid = false;
   return WG_OK;
 }
 

@@ -58,6 +58,51 @@ using namespace wgd;
 constexpr uint32_t TW = WG_TW;      // waves per workgroup
 constexpr uint32_t LPT_BINS = 130;  // round counts 0..129 (65535-B payload = 1025 blocks = 129 rounds)
 
+// AllowedIPs tables of the receive side (wg_rx.hip) as the open kernel reads them when
+// wg_open_batch is called with WG_F_RX_FILTER: one struct in device memory, rebuilt whenever a
+// filter or the slot -> filter map changes.
+constexpr uint32_t kNoFilter = 0xFFFFFFFFu;
+struct RxTables {
+  const uint32_t* slot_filter;  // per key slot: filter id or kNoFilter (NULL: no map set)
+  const uint32_t* hdr;          // per filter: root4, root6 (global node indices)
+  const uint32_t* entries;      // nodes x 256 entries: next node | bit 31 "a prefix ended in this byte"
+  uint32_t nfilters;
+  uint32_t key_slots;
+};
+
+// TransportManager.processDecryptedTransport for one opened packet whose tag verified
+// (TransportManager.java:98-119): a keepalive (len 0, :103-105), an address family that is not
+// IPv4/IPv6 or a packet too short for the destination (destinationIPOf, :124-130, throws), or a
+// destination outside the key slot's AllowedIPs (IPFilter.search, util/IPFilter.java:49-61).
+// p: the plaintext (global memory, this launch's output). Shared by k_rx_filter and the fused
+// open (WG_F_RX_FILTER).
+__device__ inline uint32_t rx_verdict(const RxTables& T, const uint8_t* p, uint32_t len, uint32_t key_slot) {
+  if (len == 0) return WG_PKT_KEEPALIVE;
+  const uint32_t ver = p[0] >> 4;
+  uint32_t nbytes, at;
+  if (ver == 4) {
+    nbytes = 4;
+    at = 16;
+  } else if (ver == 6) {
+    nbytes = 16;
+    at = 24;
+  } else {
+    return WG_PKT_BADIP;
+  }
+  if (len < at + nbytes) return WG_PKT_BADIP;
+  if (!T.slot_filter || key_slot >= T.key_slots) return WG_PKT_OK;
+  const uint32_t f = T.slot_filter[key_slot];
+  if (f == kNoFilter) return WG_PKT_OK;
+  uint32_t node = f < T.nfilters ? T.hdr[2 * f + (ver == 6 ? 1 : 0)] : 0u;  // never set: empty filter
+  bool found = false;
+  for (uint32_t L = 0; L < nbytes && node; ++L) {
+    const uint32_t e = T.entries[(size_t)node * 256 + p[at + L]];
+    found |= (e >> 31) != 0;
+    node = e & 0x7FFFFFFFu;
+  }
+  return found ? WG_PKT_OK : WG_PKT_FILTERED;
+}
+
 struct TransportParams {
   const wg_pkt* desc;
   const uint32_t* order;  // batch position -> packet index (longest first); nullptr = identity
@@ -72,6 +117,7 @@ struct TransportParams {
   const uint32_t* keys;   // device key table, 8 words per slot
   uint32_t* status;       // open: per-packet WG_PKT_*
   uint32_t prio_step;     // rounds per issue-priority level (0: no priority changes)
+  const RxTables* rx;     // open with WG_F_RX_FILTER: receive-side verdict in the status (else NULL)
 #ifdef WG_DIAG
   uint64_t* stamps;       // diagnostic build only: 10 x u64 per wave (cycles per phase, start/end times)
 #endif
@@ -313,7 +359,9 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           k[i] = kp[i];  // s_load_dwordx8
+#ifndef WG_NO_SKEY
           asm volatile("" : "+s"(k[i]));  // keep it scalar (no per-lane reload)
+#endif
         }
         uint32_t v = k[0];
 #pragma unroll
@@ -590,7 +638,14 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         }
         if constexpr (MODE == WG_MODE_OPEN) {
           bad = bcast8<0>(bad);
-          if (j == 0 && P.status) P.status[pkt] = bad ? WG_PKT_BADTAG : WG_PKT_OK;
+          if (j == 0 && P.status) {
+            uint32_t st = bad ? WG_PKT_BADTAG : WG_PKT_OK;
+            if (!bad && P.rx) {  // fused receive-side check on the plaintext this slot wrote
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's plaintext stores have landed
+              st = rx_verdict(*P.rx, outp, len, P.desc[pkt].key_slot);
+            }
+            P.status[pkt] = st;
+          }
           if (bad && valid) {  // scrub the unauthenticated plaintext written by this launch
             for (uint32_t i = j; i < len; i += 8u) outp[i] = 0;
           }

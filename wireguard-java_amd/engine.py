@@ -128,23 +128,29 @@ class Engine:
                                         out.numel(), max_len, flags,
                                         stream if stream is not None else _torch_stream()))
 
-    def open(self, desc, inp, out, status, max_len: int, uniform: bool = False, stream: int | None = None):
-        """wg_open_batch; `status` is an int32/uint32 device tensor of n entries (0 ok, 1 bad tag)."""
+    def open(self, desc, inp, out, status, max_len: int, uniform: bool = False, stream: int | None = None,
+             rx_filter: bool = False):
+        """wg_open_batch; `status` is an int32/uint32 device tensor of n entries (0 ok, 1 bad tag).
+        rx_filter (WG_F_RX_FILTER): the receive-side keepalive / IP / AllowedIPs verdict of
+        wg_rx_check(WG_RX_FILTER) written by the open kernel itself."""
         n = desc.shape[0]
+        flags = (L.WG_F_UNIFORM if uniform else 0) | (L.WG_F_RX_FILTER if rx_filter else 0)
         L.check(self._lib.wg_open_batch(self.ctx, desc.data_ptr(), n, inp.data_ptr(), inp.numel(), out.data_ptr(),
-                                        out.numel(), status.data_ptr(), max_len, L.WG_F_UNIFORM if uniform else 0,
+                                        out.numel(), status.data_ptr(), max_len, flags,
                                         stream if stream is not None else _torch_stream()))
 
     def duplex(self, seal_desc, seal_in, seal_out, seal_max_len: int, open_desc, open_in, open_out, status,
-               open_max_len: int, uniform: bool = False, frame: bool = False, stream: int | None = None):
-        """wg_duplex_batch: seal one batch and open another in one launch (the open batch must not
-        read what the seal batch writes). Same tensors as seal() / open()."""
+               open_max_len: int, uniform: bool = False, frame: bool = False, stream: int | None = None,
+               after_seal: bool = False):
+        """wg_duplex_batch: seal one batch and open another in one launch. Without after_seal the
+        open batch must not read what the seal batch writes; with it (WG_F_AFTER_SEAL) open packet i
+        is ordered after seal packet i (k_step for uniform batches). Same tensors as seal() / open()."""
         u = L.WG_F_UNIFORM if uniform else 0
         sb = L.WgBatch(seal_desc.data_ptr(), seal_in.data_ptr(), seal_out.data_ptr(), None, seal_in.numel(),
                        seal_out.numel(), seal_desc.shape[0], seal_max_len, u | (L.WG_F_FRAME if frame else 0), 0)
         ob = L.WgBatch(open_desc.data_ptr(), open_in.data_ptr(), open_out.data_ptr(),
                        status.data_ptr() if status is not None else None, open_in.numel(), open_out.numel(),
-                       open_desc.shape[0], open_max_len, u, 0)
+                       open_desc.shape[0], open_max_len, u | (L.WG_F_AFTER_SEAL if after_seal else 0), 0)
         L.check(self._lib.wg_duplex_batch(self.ctx, ctypes.byref(sb), ctypes.byref(ob),
                                           stream if stream is not None else _torch_stream()))
 

@@ -26,11 +26,20 @@ public class ChaCha20 {
 		state.asSlice(52, 12).copyFrom(nonce);
 	}
 
+	/**
+	 * Reference ChaCha20.chacha20Block (ChaCha20.java:84-104): word 12 := counter, one keystream
+	 * block into output. When both segments are native the reference hands `state` itself to
+	 * chacha_block_keystream, whose chacha_block_generic advances word 12 (chacha-generic.c:77);
+	 * with a heap segment it works on a native copy and the caller's word 12 stays `counter`.
+	 * The same side effect is reproduced here.
+	 */
 	public static void chacha20Block(MemorySegment state, MemorySegment output, int counter) {
 		state.setAtIndex(JAVA_INT, 12, counter);
 		var zeros = MemorySegment.ofArray(new byte[64]);
 		WgAead.aead(WgAead.WG_MODE_CIPHER, state.asSlice(16, 32), state.getAtIndex(JAVA_INT, 13),
 			state.getAtIndex(JAVA_INT, 14), state.getAtIndex(JAVA_INT, 15), counter, zeros, null, output.asSlice(0, 64), 64);
+		if (state.isNative() && output.isNative())
+			state.setAtIndex(JAVA_INT, 12, counter + 1);
 	}
 
 	public static void chacha20(MemorySegment key, MemorySegment nonce, MemorySegment input, MemorySegment output, int counter) {

@@ -132,9 +132,21 @@ public final class TransportBatch {
 	/** Opens {@code n} device-resident packets; status (device int32[n]) gets 0 / 1 per packet. */
 	public static void openDevice(MemorySegment table, int n, MemorySegment in, long inSize, MemorySegment out,
 	                              long outSize, MemorySegment status, int maxLen, boolean uniform, MemorySegment stream) {
+		openDevice(table, n, in, inSize, out, outSize, status, maxLen, uniform, false, stream);
+	}
+
+	/**
+	 * Opens {@code n} device-resident packets; with {@code rxFilter} (WG_F_RX_FILTER) the same launch
+	 * also applies TransportManager.processDecryptedTransport's checks (TransportManager.java:98-119:
+	 * keepalive, IP version, the key slot's AllowedIPs) and writes WG_PKT_KEEPALIVE / BADIP / FILTERED
+	 * into {@code status} for packets that verified.
+	 */
+	public static void openDevice(MemorySegment table, int n, MemorySegment in, long inSize, MemorySegment out,
+	                              long outSize, MemorySegment status, int maxLen, boolean uniform, boolean rxFilter,
+	                              MemorySegment stream) {
 		try {
 			WgAead.check((int) WgAead.OPEN_BATCH.invokeExact(WgAead.CTX, table, n, in, inSize, out, outSize, status,
-				maxLen, uniform ? WgAead.WG_F_UNIFORM : 0, stream));
+				maxLen, (uniform ? WgAead.WG_F_UNIFORM : 0) | (rxFilter ? WgAead.WG_F_RX_FILTER : 0), stream));
 		} catch (RuntimeException e) {
 			throw e;
 		} catch (Throwable e) {
@@ -152,11 +164,25 @@ public final class TransportBatch {
 	                                MemorySegment openTable, int nOpen, MemorySegment openIn, long openInSize,
 	                                MemorySegment openOut, long openOutSize, MemorySegment status, int openMaxLen,
 	                                boolean uniform, MemorySegment stream) {
+		duplexDevice(sealTable, nSeal, sealIn, sealInSize, sealOut, sealOutSize, sealMaxLen, openTable, nOpen, openIn,
+			openInSize, openOut, openOutSize, status, openMaxLen, uniform, false, stream);
+	}
+
+	/**
+	 * As above; with {@code afterSeal} (WG_F_AFTER_SEAL) the open batch reads what the seal batch writes:
+	 * open packet i is ordered after seal packet i (equal sizes). Uniform batches then run as one
+	 * k_step launch that opens each 32-packet chunk as soon as it is sealed.
+	 */
+	public static void duplexDevice(MemorySegment sealTable, int nSeal, MemorySegment sealIn, long sealInSize,
+	                                MemorySegment sealOut, long sealOutSize, int sealMaxLen,
+	                                MemorySegment openTable, int nOpen, MemorySegment openIn, long openInSize,
+	                                MemorySegment openOut, long openOutSize, MemorySegment status, int openMaxLen,
+	                                boolean uniform, boolean afterSeal, MemorySegment stream) {
 		try (var arena = Arena.ofConfined()) {
 			var s = batch(arena, sealTable, nSeal, sealIn, sealInSize, sealOut, sealOutSize, MemorySegment.NULL,
-				sealMaxLen, uniform);
+				sealMaxLen, uniform ? WgAead.WG_F_UNIFORM : 0);
 			var o = batch(arena, openTable, nOpen, openIn, openInSize, openOut, openOutSize, status, openMaxLen,
-				uniform);
+				(uniform ? WgAead.WG_F_UNIFORM : 0) | (afterSeal ? WgAead.WG_F_AFTER_SEAL : 0));
 			WgAead.check((int) WgAead.DUPLEX_BATCH.invokeExact(WgAead.CTX, s, o, stream));
 		} catch (RuntimeException e) {
 			throw e;
@@ -168,7 +194,7 @@ public final class TransportBatch {
 	// struct wg_batch {desc, in, out, status, in_size, out_size, n, max_len, flags, _reserved} (64 B)
 	private static MemorySegment batch(Arena arena, MemorySegment table, int n, MemorySegment in, long inSize,
 	                                   MemorySegment out, long outSize, MemorySegment status, int maxLen,
-	                                   boolean uniform) {
+	                                   int flags) {
 		var b = arena.allocate(WgAead.BATCH_SIZE, 8);
 		b.set(ADDRESS, 0, table);
 		b.set(ADDRESS, 8, in);
@@ -178,7 +204,7 @@ public final class TransportBatch {
 		b.set(JAVA_LONG, 40, outSize);
 		b.set(JAVA_INT, 48, n);
 		b.set(JAVA_INT, 52, maxLen);
-		b.set(JAVA_INT, 56, uniform ? WgAead.WG_F_UNIFORM : 0);
+		b.set(JAVA_INT, 56, flags);
 		b.set(JAVA_INT, 60, 0);
 		return b;
 	}

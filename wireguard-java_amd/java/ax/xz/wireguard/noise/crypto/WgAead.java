@@ -26,6 +26,9 @@ public final class WgAead {
 	public static final int WG_OK = 0;
 	public static final int WG_MODE_SEAL = 0, WG_MODE_OPEN = 1, WG_MODE_CIPHER = 2, WG_MODE_MAC = 3;
 	public static final int WG_F_UNIFORM = 1;
+	public static final int WG_F_FRAME = 2;
+	public static final int WG_F_AFTER_SEAL = 4;
+	public static final int WG_F_RX_FILTER = 8;
 	public static final int WG_PKT_OK = 0, WG_PKT_BADTAG = 1, WG_PKT_BADHDR = 2;
 	/** wg_rx_check outcomes (TransportManager.processDecryptedTransport, TransportManager.java:98-119). */
 	public static final int WG_PKT_KEEPALIVE = 3, WG_PKT_BADIP = 4, WG_PKT_FILTERED = 5, WG_PKT_REPLAY = 6;
