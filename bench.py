@@ -41,6 +41,7 @@ import argparse
 import glob
 import importlib
 import json
+import re
 import os
 import sys
 import time
@@ -134,44 +135,58 @@ def cpu_baseline(lengths, slots, counters, keys, budget_s: float = 1.5):
             "single_thread_open": round(s_open, 3)}
 
 
-def pmc_valu_insts(mode="serial"):
-    """SQ_INSTS_VALU per transport-kernel launch from the committed PMC summary: the mean of the seal
-    and open launches (serial steps), or the k_duplex launch (duplex steps; seal + open when the
-    summary has no duplex entry)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
-    if not files:
-        return None
+def _pmc_summary(workload):
+    """The newest committed PMC summary for a workload: profiles/pmc_rNN_<workload>.json as
+    tools/prof_window.py writes it (timed-window dispatches only, per-kernel entries
+    "k_transport<seal>" / "k_transport<open>" / "k_duplex"), else the older flat
+    profiles/pmc_rNN*.json (C1 only)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc_r[0-9][0-9]_{workload}.json")))
+    if files:
+        return "window", json.load(open(files[-1]))
+    if workload != "c1":
+        return None, None
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "pmc_r[0-9][0-9]*.json"))
+                   if not re.search(r"_c\d\.json$", f))
+    return ("flat", json.load(open(files[-1]))) if files else (None, None)
+
+
+def _pmc_value(workload, mode, get, flat_get):
+    """Per-launch value of a counter-derived figure: the mean of the seal and open launches (serial
+    and step modes launch both kernels per step), or the k_duplex launch (duplex mode)."""
     try:
-        d = json.load(open(files[-1]))
-        if mode == "step":
-            return d["step"]["counters_mean"]["SQ_INSTS_VALU"] if "step" in d else None
+        fmt, d = _pmc_summary(workload)
+        if fmt == "window":
+            if mode == "duplex":
+                return get(d["k_duplex"]) if "k_duplex" in d else None
+            v = [get(d[k]) for k in ("k_transport<seal>", "k_transport<open>") if k in d]
+            return sum(v) / 2 if len(v) == 2 else None
+        if fmt == "flat":
+            return flat_get(d, mode)
+    except (KeyError, TypeError, ValueError, OSError):
+        return None
+    return None
+
+
+def pmc_valu_insts(workload="c1", mode="serial"):
+    """SQ_INSTS_VALU per transport-kernel launch from the committed PMC summary."""
+    def flat(d, mode):
         if mode == "duplex" and "duplex" in d:
             return d["duplex"]["counters_mean"]["SQ_INSTS_VALU"]
         v = [d[k]["counters_mean"]["SQ_INSTS_VALU"] for k in ("seal", "open") if k in d]
         return (sum(v) if mode == "duplex" else sum(v) / len(v)) if len(v) == 2 else None
-    except Exception:
-        return None
+    return _pmc_value(workload, mode, lambda e: e["counters_mean"]["SQ_INSTS_VALU"], flat)
 
 
-def pmc_traffic(mode="serial"):
-    """Per-launch HBM bytes of the transport kernel (mean of the seal and open launches, or the
-    k_duplex launch) from the newest committed PMC summary (profiles/pmc_*.json, written by
-    tools/pmc_to_json.py)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")))
-    if not files:
-        return None
-    try:
-        d = json.load(open(files[-1]))
-        if mode == "step":
-            return round(d["step_hbm_bytes_per_launch"]) if "step_hbm_bytes_per_launch" in d else None
+def pmc_traffic(workload="c1", mode="serial"):
+    """Per-launch HBM bytes of the transport kernel from the committed PMC summary (FETCH_SIZE and
+    WRITE_SIZE passes with the gfx950 corrections, see tools/prof_window.py)."""
+    def flat(d, mode):
         if mode == "duplex" and "duplex_hbm_bytes_per_launch" in d:
-            return round(d["duplex_hbm_bytes_per_launch"])
+            return d["duplex_hbm_bytes_per_launch"]
         v = [d[k] for k in ("seal_hbm_bytes_per_launch", "open_hbm_bytes_per_launch") if k in d]
-        if len(v) != 2:
-            return None
-        return round(sum(v)) if mode == "duplex" else round(sum(v) / 2)
-    except Exception:
-        return None
+        return None if len(v) != 2 else sum(v) if mode == "duplex" else sum(v) / 2
+    v = _pmc_value(workload, mode, lambda e: e["hbm_bytes_per_launch"], flat)
+    return round(v) if v is not None else None
 
 
 def host_bench(args):
@@ -475,8 +490,8 @@ def main():
     # seal reads L, writes L+16; open reads L+16, writes L -> 4L+32 per packet
     step_alg = float((4 * lengths + 32).sum())
     achieved = step_alg / (gpu_step_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(args.mode) if args.workload == "c1" else None
-    valu = pmc_valu_insts(args.mode) if args.workload == "c1" else None
+    traffic = pmc_traffic(args.workload, args.mode)
+    valu = pmc_valu_insts(args.workload, args.mode)
 
     if args.mode == "duplex":
         kname = "k_duplex (seal + open halves)"

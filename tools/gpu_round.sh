@@ -4,15 +4,18 @@
 #   the UDP host pipeline, receive-side and per-packet timings, rocprofv3 kernel traces of the
 #   C1 and C2 bench commands (tools/prof_window.py keeps the timed region only) and one PMC pass
 #   per counter group for C1 and C2 (each pass its own run, as the MI355X guide prescribes).
-# Usage: bash tools/gpu_round.sh r03 [quick]
+# Usage: bash tools/gpu_round.sh r03 [bench|prof|all] (bench: everything up to the profiles; prof: the
+# rocprofv3 traces and PMC passes; one gpurun call each fits the 600-s call limit)
 set -o pipefail
 R=${1:-r03}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$ROOT/gpurun_out/$R
 mkdir -p $O $O/pmc
 cd $ROOT
+PART=${2:-all}
 step() { echo "[round] $1"; }
 die() { echo "[round] FAILED: $1 (rc $2)"; exit $2; }
+if [ "$PART" != prof ]; then
 step tests
 timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 || die tests $?
 tail -1 $O/gpu_tests.log
@@ -27,21 +30,19 @@ timeout -k 10 300 python bench.py --mode serial --no-cpu-baseline > $O/bench_c1_
 step "bench c2"
 timeout -k 10 300 python bench.py --workload c2 > $O/bench_c2.json 2>> $O/bench.err || die bench_c2 $?
 cat $O/bench_c2.json
-if [ "$2" != "quick" ]; then
-  step "bench c3"
-  timeout -k 10 400 python bench.py --workload c3 --no-cpu-baseline --steps 5 --warmup 1 > $O/bench_c3.json 2>> $O/bench.err || die bench_c3 $?
-  cat $O/bench_c3.json
-  step "host path c4"
-  timeout -k 10 300 python bench.py --workload c4 --steps 5 --warmup 1 > $O/bench_c4_pinned.json 2>> $O/bench.err || die c4 $?
-  WG_HOST_PATH=copy timeout -k 10 300 python bench.py --workload c4 --steps 5 --warmup 1 > $O/bench_c4_pinned_copy.json 2>> $O/bench.err || die c4copy $?
-  timeout -k 10 300 python bench.py --workload c4 --host-mem pageable --steps 3 --warmup 1 > $O/bench_c4_pageable.json 2>> $O/bench.err || die c4pageable $?
-  cat $O/bench_c4_*.json
-  step "host-to-host pipeline (UDP loopback)"
-  for k in 1 8; do
-    timeout -k 10 200 ./tools/host_pipeline --backend gpu --packets 65536 --reps 5 --udp-streams $k --tun >> $O/host_pipeline_gpu.jsonl || die pipeline $?
-  done
-  timeout -k 10 300 ./tools/host_pipeline --backend cpu --oracle oracle/liboracle.so --threads 16 --packets 65536 --reps 3 --udp-streams 8 --tun >> $O/host_pipeline_cpu.jsonl || die pipeline_cpu $?
-fi
+step "bench c3"
+timeout -k 10 400 python bench.py --workload c3 --no-cpu-baseline --steps 5 --warmup 1 > $O/bench_c3.json 2>> $O/bench.err || die bench_c3 $?
+cat $O/bench_c3.json
+step "host path c4"
+timeout -k 10 300 python bench.py --workload c4 --steps 5 --warmup 1 > $O/bench_c4_pinned.json 2>> $O/bench.err || die c4 $?
+WG_HOST_PATH=copy timeout -k 10 300 python bench.py --workload c4 --steps 5 --warmup 1 > $O/bench_c4_pinned_copy.json 2>> $O/bench.err || die c4copy $?
+timeout -k 10 300 python bench.py --workload c4 --host-mem pageable --steps 3 --warmup 1 > $O/bench_c4_pageable.json 2>> $O/bench.err || die c4pageable $?
+cat $O/bench_c4_*.json
+step "host-to-host pipeline (UDP loopback)"
+for k in 1 8; do
+  timeout -k 10 200 ./tools/host_pipeline --backend gpu --packets 65536 --reps 5 --udp-streams $k --tun >> $O/host_pipeline_gpu.jsonl || die pipeline $?
+done
+timeout -k 10 300 ./tools/host_pipeline --backend cpu --oracle oracle/liboracle.so --threads 16 --packets 65536 --reps 3 --udp-streams 8 --tun >> $O/host_pipeline_cpu.jsonl || die pipeline_cpu $?
 step "receive side"
 timeout -k 10 180 python tools/bench_rx.py > $O/rx_timing.json || die rx $?
 cat $O/rx_timing.json
@@ -50,6 +51,8 @@ for t in 1 16 64; do timeout -k 10 120 ./tools/batcher_bench $t $((t == 1 ? 4000
 timeout -k 10 120 ./tools/batcher_bench 16 10000 0 >> $O/batcher.jsonl || die batcher_mixed $?
 cat $O/batcher.jsonl
 timeout -k 10 120 ./tools/pp_stamps 1420 > $O/pp_stamps.json || die pp_stamps $?
+fi
+[ "$PART" = bench ] && { step done; exit 0; }
 cd /tmp && export TMPDIR=/tmp
 for w in c1 c2; do
   step "rocprofv3 kernel trace $w"
@@ -59,7 +62,7 @@ for w in c1 c2; do
   for grp in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE"; do
     i=$((i+1))
     step "pmc $w $grp"
-    timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d $O/pmc/${w}_p$i -o run --output-format csv -- python3 $ROOT/bench.py --workload $w --no-cpu-baseline --steps 20 --warmup 2 > $O/pmc/${w}_p$i.json 2> $O/pmc/${w}_p$i.log || die pmc_$w_$i $?
+    timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d $O/pmc/${w}_p$i -o run --output-format csv -- python3 $ROOT/bench.py --workload $w --no-cpu-baseline --steps 20 --warmup 2 > $O/pmc/${w}_p$i.json 2> $O/pmc/${w}_p$i.log || die pmc_${w}_$i $?
   done
   args=""
   for j in 1 2 3 4; do args="$args $(find $O/pmc/${w}_p$j -name '*counter_collection.csv' | head -1) $O/pmc/${w}_p$j.json"; done

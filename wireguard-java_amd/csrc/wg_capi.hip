@@ -415,15 +415,18 @@ hipStream_t pick_stream(wg_ctx*, void* stream) { return (hipStream_t)stream; }
 int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStream_t s) {
   const bool same_plan = sb->max_len == ob->max_len && (sb->flags & WG_F_UNIFORM) == (ob->flags & WG_F_UNIFORM) &&
                          c->resident_waves[0] == c->resident_waves[1];
+  // a uniform batch is not ordered (one packet per slot): no workspace, and no event record
+  // between one step's open and the next step's seal
+  const bool ordered = !(sb->flags & WG_F_UNIFORM) || !(ob->flags & WG_F_UNIFORM);
   int rc;
-  if ((rc = ws_acquire(c, s)) != WG_OK) return rc;
+  if (ordered && (rc = ws_acquire(c, s)) != WG_OK) return rc;
   rc = launch_transport<WG_MODE_SEAL>(c, sb->desc, sb->n, sb->in, sb->in_size, sb->out, sb->out_size, nullptr,
                                       sb->max_len, sb->flags, s, nullptr, &c->lpt_hist, &c->lpt_order);
   if (rc == WG_OK)
     rc = launch_transport<WG_MODE_OPEN>(c, ob->desc, ob->n, ob->in, ob->in_size, ob->out, ob->out_size, ob->status,
                                         ob->max_len, ob->flags & ~WG_F_AFTER_SEAL, s, nullptr, &c->lpt_hist,
                                         &c->lpt_order, same_plan);
-  const int rr = ws_release(c, s);
+  const int rr = ordered ? ws_release(c, s) : WG_OK;
   return rc != WG_OK ? rc : rr;
 }
 
