@@ -141,6 +141,49 @@ def test_per_packet_edges_bit_exact():
 
 
 @pytest.mark.gpu
+def test_new_context_while_another_server_runs():
+    """A context created while another context's per-packet server is resident: its key table
+    is zeroed on its own stream, so the first wg_keys_set is not overwritten by a late
+    zero-fill (found on the box: every tag of the first batch came from the all-zero key).
+    Also reports how long a batch launch takes while the server is resident."""
+    import torch
+    W = wg()
+    a = W.Engine(0, key_slots=2)
+    b = None
+    try:
+        a.batcher_config(waves=4, idle_us=300000)  # keep the server resident for the whole test
+        ka = splitmix_bytes(1950, 32)
+        a.set_keys(0, ka)
+        pt = splitmix_bytes(1951, 100)
+        assert a.seal1(0, 1, pt) == O.c_aead_seal(ka, O.transport_nonce(1), pt)
+        b = W.Engine(0, key_slots=8)
+        keys = splitmix_np(1952, 32 * 3)
+        b.set_keys(0, keys.tobytes())
+        n = 300
+        dev = torch.device("cuda", 0)
+        off = np.arange(n, dtype=np.uint64) * 32
+        desc = W.pack_desc(off, off, np.arange(n, dtype=np.uint64) + 7, np.zeros(n, np.int64), np.arange(n) % 3)
+        d = torch.from_numpy(W.desc_as_int64(desc)).to(dev)
+        inp = torch.zeros(32 * n, dtype=torch.uint8, device=dev)
+        out = torch.zeros(32 * n, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        b.seal(d, inp, out, 0, uniform=True)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        got = out.cpu().numpy()
+        for i in range(n):
+            k = keys[32 * (i % 3):32 * (i % 3) + 32].tobytes()
+            assert got[32 * i:32 * i + 16].tobytes() == O.c_aead_seal(k, O.transport_nonce(i + 7), b""), i
+        print(f"batch seal while another context's server is resident: {dt * 1e3:.2f} ms")
+        assert a.seal1(0, 2, pt) == O.c_aead_seal(ka, O.transport_nonce(2), pt)
+    finally:
+        if b is not None:
+            b.close()
+        a.close()
+
+
+@pytest.mark.gpu
 def test_failed_server_launch_is_not_sticky(monkeypatch):
     """A failed launch of the per-packet server fails only the call that hit it; the next
     call launches again and succeeds (test hook WG_PP_TEST_FAIL_LAUNCHES)."""

@@ -488,7 +488,11 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpo, wgt::k_transport<WG_MODE_OPEN>, 64 * wgt::TW, 0) !=
           hipSuccess ||
       hipMalloc(&c->keys, (size_t)key_slots * 32) != hipSuccess ||
-      hipMemset(c->keys, 0, (size_t)key_slots * 32) != hipSuccess) {
+      // on the context's stream, like every later key write: a memset on the null stream can sit
+      // behind another context's per-packet server in a shared hardware queue and land AFTER the
+      // first wg_keys_set (which runs on this non-blocking stream), zeroing the keys it wrote
+      hipMemsetAsync(c->keys, 0, (size_t)key_slots * 32, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess) {
     wg_ctx_destroy(c);
     return fail(WG_ENOMEM, "context allocation failed on device %d", device);
   }
@@ -506,8 +510,9 @@ int wg_ctx_destroy(wg_ctx* c) {
   DeviceGuard g(c->device);
   rx_free(c);
   if (c->keys) {
-    (void)hipMemset(c->keys, 0, (size_t)c->key_slots * 32);  // SymmetricKeypair.clean zeroes keys
-    (void)hipDeviceSynchronize();
+    (void)hipDeviceSynchronize();  // no launch of this context may still read the table
+    (void)hipMemsetAsync(c->keys, 0, (size_t)c->key_slots * 32, c->stream);  // SymmetricKeypair.clean zeroes keys
+    (void)hipStreamSynchronize(c->stream);
     (void)hipFree(c->keys);
   }
   for (auto& e : c->events) {

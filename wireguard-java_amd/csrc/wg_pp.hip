@@ -351,7 +351,8 @@ int pp_get(wg_ctx* c, PPServer** out) {
     // wave w starts at ticket w (tickets t = w mod W belong to wave w)
     uint64_t nx[wgpp::kMaxWaves];
     for (uint32_t w = 0; w < wgpp::kMaxWaves; ++w) nx[w] = w;
-    ok = hipMemcpy(S->d_next, nx, sizeof nx, hipMemcpyHostToDevice) == hipSuccess;
+    ok = hipMemcpyAsync(S->d_next, nx, sizeof nx, hipMemcpyHostToDevice, S->stream) == hipSuccess &&
+         hipStreamSynchronize(S->stream) == hipSuccess;  // not the null stream (see wg_ctx_create)
   }
   if (!ok) {
     pp_free(S);
@@ -520,7 +521,8 @@ int wg_batcher_config(wg_ctx* c, uint32_t waves, uint32_t idle_us) {
     uint64_t nx[wgpp::kMaxWaves];
     for (uint32_t w = 0; w < wgpp::kMaxWaves; ++w) nx[w] = base + (w + waves - base % waves) % waves;
     DeviceGuard dg(c->device);
-    HIPTRY(hipMemcpy(S->d_next, nx, sizeof nx, hipMemcpyHostToDevice));
+    HIPTRY(hipMemcpyAsync(S->d_next, nx, sizeof nx, hipMemcpyHostToDevice, S->stream));
+    HIPTRY(hipStreamSynchronize(S->stream));
     S->waves = waves;
   }
   S->idle_us = idle_us ? idle_us : 20000;

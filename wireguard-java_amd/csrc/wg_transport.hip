@@ -569,7 +569,11 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
             uint4 v = make_uint4(acc[0] ^ t, acc[1], acc[2] + c0, acc[3]);
 #endif
             // acc is still 0 before a packet's first chunk (round 0, t = 0): no product needed
+#ifdef WG_HORNER_CHAIN
+            if (round != 0 || t != 0) poly_mul(acc, R, Rs);
+#else
             if (round != 0 || t != 0) poly_mul_ilp(acc, R, Rs);
+#endif
             uint32_t cl[5];
             poly_block_limbs(v.x, v.y, v.z, v.w, 1u << 24, cl);
 #pragma unroll
