@@ -265,31 +265,6 @@ __device__ __forceinline__ void poly_mul(uint32_t h[5], const uint32_t r[5], con
 }
 #endif
 
-// Same product with the five limb sums as independent v_mad_u64_u32 chains
-// (ILP 5) and the carries applied afterwards with 64-bit adds: more instructions
-// than poly_mul, a much shorter dependent chain.
-__device__ __forceinline__ void poly_mul_ilp(uint32_t h[5], const uint32_t r[5], const uint32_t s[5]) {
-  uint64_t d0 = (uint64_t)h[0] * r[0] + (uint64_t)h[1] * s[4] + (uint64_t)h[2] * s[3] + (uint64_t)h[3] * s[2] +
-                (uint64_t)h[4] * s[1];
-  uint64_t d1 = (uint64_t)h[0] * r[1] + (uint64_t)h[1] * r[0] + (uint64_t)h[2] * s[4] + (uint64_t)h[3] * s[3] +
-                (uint64_t)h[4] * s[2];
-  uint64_t d2 = (uint64_t)h[0] * r[2] + (uint64_t)h[1] * r[1] + (uint64_t)h[2] * r[0] + (uint64_t)h[3] * s[4] +
-                (uint64_t)h[4] * s[3];
-  uint64_t d3 = (uint64_t)h[0] * r[3] + (uint64_t)h[1] * r[2] + (uint64_t)h[2] * r[1] + (uint64_t)h[3] * r[0] +
-                (uint64_t)h[4] * s[4];
-  uint64_t d4 = (uint64_t)h[0] * r[4] + (uint64_t)h[1] * r[3] + (uint64_t)h[2] * r[2] + (uint64_t)h[3] * r[1] +
-                (uint64_t)h[4] * r[0];
-  uint32_t c;
-  c = (uint32_t)(d0 >> 26); h[0] = (uint32_t)d0 & M26; d1 += c;
-  c = (uint32_t)(d1 >> 26); h[1] = (uint32_t)d1 & M26; d2 += c;
-  c = (uint32_t)(d2 >> 26); h[2] = (uint32_t)d2 & M26; d3 += c;
-  c = (uint32_t)(d3 >> 26); h[3] = (uint32_t)d3 & M26; d4 += c;
-  c = (uint32_t)(d4 >> 26); h[4] = (uint32_t)d4 & M26;
-  h[0] += c * 5u;
-  c = h[0] >> 26; h[0] &= M26;
-  h[1] += c;
-}
-
 __device__ __forceinline__ void poly_scale5(const uint32_t r[5], uint32_t s[5]) {
   s[0] = 0;
   s[1] = r[1] * 5u; s[2] = r[2] * 5u; s[3] = r[3] * 5u; s[4] = r[4] * 5u;

@@ -19,8 +19,10 @@
 // lanes 1..3 of a slot compute it once per packet and every block takes it by ds_swizzle
 // broadcast (chacha20_block_hoisted: -3% VALU instructions on C1). Poly1305: the length block
 // is written into the image by the lane whose counter block holds it, so the Horner steps
-// read it like ciphertext; each step's product runs as five independent v_mad_u64_u32
-// chains (poly_mul_ilp: +1% instructions, no slower on C1, +3% on C2's mixed lengths). The
+// read it like ciphertext; each step's product chains every limb's carry into the next limb's
+// v_mad_u64_u32 accumulator (poly_mul: 5 fewer instructions per step than five independent
+// chains with the carries added afterwards; C1 +1.2%, C2 +0.2% in round 3, where round 2's
+// kernel had measured the independent chains +3% on C2). The
 // r-power scan and the slot sum exchange limbs through DPP (row_shr / quad_perm), which stays
 // in the VALU instead of an LDS round trip in the middle of a dependent chain.
 // Slots are persistent: slot g of S processes batch positions g, 2S-1-g, 2S+g, ... (a
@@ -569,11 +571,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
             uint4 v = make_uint4(acc[0] ^ t, acc[1], acc[2] + c0, acc[3]);
 #endif
             // acc is still 0 before a packet's first chunk (round 0, t = 0): no product needed
-#ifdef WG_HORNER_CHAIN
             if (round != 0 || t != 0) poly_mul(acc, R, Rs);
-#else
-            if (round != 0 || t != 0) poly_mul_ilp(acc, R, Rs);
-#endif
             uint32_t cl[5];
             poly_block_limbs(v.x, v.y, v.z, v.w, 1u << 24, cl);
 #pragma unroll
