@@ -152,15 +152,18 @@ def _pmc_summary(workload):
 
 def _pmc_value(workload, mode, get, flat_get):
     """Per-launch value of a counter-derived figure: the mean of the seal and open launches (serial
-    and step modes launch both kernels per step), or the k_duplex launch (duplex mode)."""
+    mode, or a step as two launches), the k_duplex launch (duplex mode) or the k_step launch
+    (mode "fused": one WG_F_AFTER_SEAL step)."""
     try:
         fmt, d = _pmc_summary(workload)
         if fmt == "window":
             if mode == "duplex":
                 return get(d["k_duplex"]) if "k_duplex" in d else None
+            if mode == "fused":
+                return get(d["k_step"]) if "k_step" in d else None
             v = [get(d[k]) for k in ("k_transport<seal>", "k_transport<open>") if k in d]
             return sum(v) / 2 if len(v) == 2 else None
-        if fmt == "flat":
+        if fmt == "flat" and mode != "fused":
             return flat_get(d, mode)
     except (KeyError, TypeError, ValueError, OSError):
         return None
@@ -317,6 +320,8 @@ def main():
     # longest-first once for both); serial: wg_seal_batch, then wg_open_batch
     ap.add_argument("--mode", default="step", choices=["step", "serial", "duplex"])
     ap.add_argument("--kernel", default="default", help="transport kernel (wg_ctx_set_kernel): default|wave1|tile")
+    # --variant 1: a WG_F_AFTER_SEAL step as two launches (seal, then open) instead of one k_step launch
+    ap.add_argument("--variant", type=int, default=0, choices=[0, 1])
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -345,7 +350,7 @@ def main():
     n = len(lengths)
     keys = splitmix_np(0xC0FFEE + rank, 32 * nkeys)
     eng = wg.Engine(local, key_slots=max(nkeys, 1))
-    eng.set_kernel(args.kernel)
+    eng.set_kernel(args.kernel, variant=args.variant if args.kernel in ("default", "transport") else 0)
     eng.set_keys(0, keys.tobytes())
 
     # layout: packets at 16-byte aligned strides; pt buffer, ct||tag buffer, decrypted pt buffer
@@ -473,7 +478,9 @@ def main():
 
     payload = 2.0 * float(lengths.sum())  # sealed + opened bytes per step on this rank
     D = importlib.import_module("wireguard-java_amd.dist")
-    launches = 1 if args.mode == "duplex" else 2  # transport kernel launches per step
+    # transport kernel launches per step: k_duplex, or k_step (one WG_F_AFTER_SEAL step), or seal + open
+    fused_step = args.mode == "step" and args.kernel in ("default", "transport") and args.variant == 0
+    launches = 1 if (args.mode == "duplex" or fused_step) else 2
     # this rank's own figures, gathered before the max-over-ranks reduction (BASELINE configs[3]:
     # per-GPU and aggregate GiB/s)
     per_gpu = D.gather_per_rank(dist if world > 1 else None, dev, {
@@ -490,12 +497,16 @@ def main():
     # seal reads L, writes L+16; open reads L+16, writes L -> 4L+32 per packet
     step_alg = float((4 * lengths + 32).sum())
     achieved = step_alg / (gpu_step_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(args.workload, args.mode)
-    valu = pmc_valu_insts(args.workload, args.mode)
+    pmc_mode = "fused" if fused_step else args.mode
+    traffic = pmc_traffic(args.workload, pmc_mode)
+    valu = pmc_valu_insts(args.workload, pmc_mode)
 
     if args.mode == "duplex":
         kname = "k_duplex (seal + open halves)"
         knames = ["k_duplex"]
+    elif fused_step:
+        kname = "k_step (seal, then open of the same packets, per wave)"
+        knames = ["k_step"]
     else:
         kname = "k_transport<SEAL|OPEN>" if args.kernel == "default" else args.kernel
         base = {"default": "k_transport", "transport": "k_transport", "wave1": "k_wave", "tile": "k_tile"}[args.kernel]

@@ -114,8 +114,10 @@ const char* wg_version(void);
  * (a test and A/B hook beside the reference interface). name: "default"
  * or NULL or "transport" (k_transport, the product kernel), "wave1" (the round-1
  * k_wave kernel, kept as the performance baseline) or "tile" (k_tile, the general
- * AEAD kernel run on transport descriptors). lanes and variant are ignored (kept for
- * ABI stability). Every kernel computes identical bytes; they differ only in speed. */
+ * AEAD kernel run on transport descriptors). lanes is ignored (kept for ABI stability).
+ * variant (transport kernel only): 0 = a WG_F_AFTER_SEAL step is ONE k_step launch (each wave
+ * seals its packets, then opens them); 1 = the same step as two launches, seal then open.
+ * Every kernel and variant computes identical bytes; they differ only in speed. */
 int wg_ctx_set_kernel(wg_ctx* ctx, const char* name, uint32_t lanes, uint32_t variant);
 
 /* ---- keys: SymmetricKeypair(byte[] send, byte[] recv) and clean() ---------
@@ -170,9 +172,13 @@ int wg_open_batch(wg_ctx* ctx, const wg_pkt* desc_dev, uint32_t n, const uint8_t
  * open->flags: WG_F_UNIFORM, WG_F_AFTER_SEAL; open->status is required when open->n > 0.
  * Either n may be 0.
  * WG_F_AFTER_SEAL (open->flags): the open batch DOES read what the seal batch writes: open packet i
- *   is ordered after seal packet i (same n in both batches; e.g. a loopback or a verify pass over
- *   what was just sealed). The seal launch and then the open launch run on `stream`; a mixed-length
- *   batch is ordered longest-first once, for both (its packets have the same lengths). */
+ *   is ordered after seal packet i, and after no other seal packet, so it may read what seal packet
+ *   i writes but not what another seal packet of the call writes (same n in both batches; e.g. two
+ *   peers in loopback, or a verify pass over what was just sealed). With the transport kernel and
+ *   equal max_len / WG_F_UNIFORM on both sides (and no WG_F_FRAME) the step is ONE k_step launch in
+ *   which every wave seals its packets and then opens the same batch positions; otherwise the seal
+ *   launch and then the open launch run on `stream`. A mixed-length batch is ordered longest-first
+ *   once, for both (its packets have the same lengths). */
 #define WG_F_AFTER_SEAL 4u
 typedef struct wg_batch {
   const wg_pkt* desc; /* device, 16-byte aligned */

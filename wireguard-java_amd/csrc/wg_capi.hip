@@ -93,7 +93,11 @@ struct wg_ctx {
   uint32_t key_slots = 0;
   uint32_t* keys = nullptr;               // device key table
   const uint32_t* receivers = nullptr;    // device receiver_index per key slot (WG_F_FRAME; caller-owned)
-  uint32_t resident_waves[2] = {0, 0};    // k_transport<SEAL/OPEN> waves resident at once (occupancy)
+  // waves resident at once (occupancy) of k_transport<SEAL>, <OPEN> and k_step, with 8-lane [0] and
+  // 16-lane [1] slots
+  uint32_t resident_waves[2][3] = {{0, 0, 0}, {0, 0, 0}};
+  int slot16 = 1;                         // 16-lane slots for mixed-length batches (WG_SLOT16=0: never)
+  bool step_two_launches = false;         // wg_ctx_set_kernel variant 1: WG_F_AFTER_SEAL as seal + open launches
   // plan workspace: k_tile block scan, k_transport longest-first order
   DevBuf plan_nb, plan_prefix, plan_tiles, plan_ntiles, plan_tmp, lpt_hist, lpt_order;
   DevBuf lpt_hist2, lpt_order2;  // the open half of a wg_duplex_batch
@@ -279,13 +283,14 @@ int launch_tiles(wg_ctx* c, const void* desc, uint32_t n, const uint8_t* in, uin
   return ws_release(c, s);
 }
 
-// Parameters and grid of one k_transport direction (shared by k_transport and k_duplex):
+// Parameters and grid of one k_transport direction (shared by k_transport, k_step and k_duplex):
 // persistent slots for mixed lengths (longest-first order in lpt_order), one packet per
-// slot for uniform batches. cap_slots: the slots resident at once for this direction.
+// slot for uniform batches. cap_waves: the waves resident at once for this direction; G: lanes
+// per slot (64 / G slots per wave).
 template <int MODE>
 int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, uint64_t in_size, uint8_t* out,
                    uint64_t out_size, uint32_t* status, uint32_t max_len, uint32_t flags, hipStream_t s,
-                   uint64_t cap_slots, DevBuf& lpt_hist, DevBuf& lpt_order, wgt::TransportParams* Pout,
+                   uint64_t cap_waves, uint32_t G, DevBuf& lpt_hist, DevBuf& lpt_order, wgt::TransportParams* Pout,
                    uint32_t* grid_out, bool* ordered_out, const wgt::RxTables* rx = nullptr,
                    bool private_ws = false, bool reuse_order = false) {
   bool ordered = false;
@@ -304,6 +309,8 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
 #ifdef WG_DIAG
   P.stamps = g_stamps;
 #endif
+  const uint32_t spw = 64u / G;  // slots per wave
+  const uint64_t cap_slots = spw * cap_waves;
   uint64_t per_slot = (n + cap_slots - 1) / cap_slots;
   // mixed lengths: a slot holding one packet runs as long as the longest packet, so once a
   // one-packet-per-slot grid would fill more than half the machine, pair packets longest-first
@@ -317,13 +324,13 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   // per slot with longest-first order measured 13% slower on C2)
   if (flags & WG_F_UNIFORM) per_slot = 1;
 #endif
-  const uint32_t waves = (uint32_t)((n + 8ull * per_slot - 1) / (8ull * per_slot));
+  const uint32_t waves = (uint32_t)((n + spw * per_slot - 1) / (spw * per_slot));
   const uint32_t grid = (waves + wgt::TW - 1) / wgt::TW;
-  P.slots = grid * wgt::TW * 8u;
+  P.slots = grid * wgt::TW * spw;
   // mixed lengths: the rounds a slot runs, spread over the 4 issue-priority levels (k_transport),
   // so the waves that have done the least work issue first (C2 +2%); uniform batches keep the
   // default oldest-first arbitration (the same schedule cost C1 2%)
-  const uint32_t max_rounds = (host_pkt_blocks<WG_MODE_SEAL>(max_len) + 7u) / 8u;
+  const uint32_t max_rounds = (host_pkt_blocks<WG_MODE_SEAL>(max_len) + G - 1u) / G;
   P.prio_step = (flags & WG_F_UNIFORM) ? 0u : std::max<uint32_t>(1u, (uint32_t)((per_slot * max_rounds + 3u) / 4u));
   if (!(flags & WG_F_UNIFORM) && per_slot > 1) {  // longest-first order (LPT) for the snake
     // reuse_order: the order already in lpt_order (the seal of the same packets, WG_F_AFTER_SEAL);
@@ -349,7 +356,11 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   return WG_OK;
 }
 
-// Transport seal/open through k_transport: persistent slots, 8 per wave. Each slot takes
+// Lanes per slot of k_transport / k_step for a batch: 16 for mixed lengths (long packets take half
+// as many rounds, so the longest-first pairs fill 8 waves per SIMD), 8 for uniform batches.
+uint32_t slot_lanes(const wg_ctx* c, uint32_t flags) { return !(flags & WG_F_UNIFORM) && c->slot16 ? 16u : 8u; }
+
+// Transport seal/open through k_transport: persistent slots, 64 / G per wave. Each slot takes
 // ceil(n / resident slots) packets; mixed-length batches are ordered longest-first on
 // the device first (k_lpt_*), so the slots' snake over the order balances their rounds.
 template <int MODE>
@@ -390,16 +401,18 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
   wgt::TransportParams P{};
   uint32_t grid = 0;
   bool ordered = false;
-  const uint64_t cap_slots = 8ull * std::max<uint32_t>(c->resident_waves[MODE == WG_MODE_OPEN], wgt::TW);
+  const uint32_t G = slot_lanes(c, flags);
+  const uint64_t cap_waves = std::max<uint32_t>(c->resident_waves[G == 16][MODE == WG_MODE_OPEN], wgt::TW);
   if (rx && c->kern != KERN_TRANSPORT) return fail(WG_EINVAL, "WG_F_RX_FILTER needs the transport kernel");
   const bool own = own_hist && own_order;  // the caller holds the plan workspace (launch_after_seal)
-  int rc = plan_transport<MODE>(c, desc, n, in, in_size, out, out_size, status, max_len, flags, s, cap_slots,
+  int rc = plan_transport<MODE>(c, desc, n, in, in_size, out, out_size, status, max_len, flags, s, cap_waves, G,
                                 own ? *own_hist : c->lpt_hist, own ? *own_order : c->lpt_order, &P, &grid, &ordered,
                                 rx, own, reuse_order);
   if (rc != WG_OK) return rc;
   hipEvent_t ev;
   record_start(c, s, &ev);
-  hipLaunchKernelGGL((wgt::k_transport<MODE>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
+  if (G == 16) hipLaunchKernelGGL((wgt::k_transport<MODE, 16>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
+  else hipLaunchKernelGGL((wgt::k_transport<MODE, 8>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
   const hipError_t e = hipGetLastError();
   record_end(c, s, ev);
   if (e != hipSuccess) return fail(WG_EDEVICE, "k_transport launch: %s", hipGetErrorString(e));
@@ -414,18 +427,57 @@ hipStream_t pick_stream(wg_ctx*, void* stream) { return (hipStream_t)stream; }
 // plan workspace is held from the seal's order to the open. Caller holds c->mu.
 int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStream_t s) {
   const bool same_plan = sb->max_len == ob->max_len && (sb->flags & WG_F_UNIFORM) == (ob->flags & WG_F_UNIFORM) &&
-                         c->resident_waves[0] == c->resident_waves[1];
+                         c->resident_waves[0][0] == c->resident_waves[0][1] &&
+                         c->resident_waves[1][0] == c->resident_waves[1][1];
   // a uniform batch is not ordered (one packet per slot): no workspace, and no event record
   // between one step's open and the next step's seal
   const bool ordered = !(sb->flags & WG_F_UNIFORM) || !(ob->flags & WG_F_UNIFORM);
+  // one k_step launch: both halves on one grid and one order, so every slot opens what it sealed
+  const bool fused = c->kern == KERN_TRANSPORT && !c->step_two_launches && sb->max_len == ob->max_len &&
+                     (sb->flags & WG_F_UNIFORM) == (ob->flags & WG_F_UNIFORM) && !(sb->flags & WG_F_FRAME);
+  if (fused) {
+    if (sb->n == 0) return WG_OK;
+    for (const wg_batch* b : {sb, ob}) {
+      if (!b->desc || (((uintptr_t)b->desc) & 15u))
+        return fail(WG_EINVAL, "descriptor array must be non-NULL and 16-byte aligned");
+      if (!b->in || !b->out) return fail(WG_EINVAL, "NULL buffer");
+      if (b->max_len > WG_MAX_PACKET) return fail(WG_E2BIG, "max_len %u > WG_MAX_PACKET", b->max_len);
+    }
+  }
   int rc;
   if (ordered && (rc = ws_acquire(c, s)) != WG_OK) return rc;
-  rc = launch_transport<WG_MODE_SEAL>(c, sb->desc, sb->n, sb->in, sb->in_size, sb->out, sb->out_size, nullptr,
-                                      sb->max_len, sb->flags, s, nullptr, &c->lpt_hist, &c->lpt_order);
-  if (rc == WG_OK)
-    rc = launch_transport<WG_MODE_OPEN>(c, ob->desc, ob->n, ob->in, ob->in_size, ob->out, ob->out_size, ob->status,
-                                        ob->max_len, ob->flags & ~WG_F_AFTER_SEAL, s, nullptr, &c->lpt_hist,
-                                        &c->lpt_order, same_plan);
+  if (fused) {
+    const uint32_t G = slot_lanes(c, sb->flags);
+    const uint64_t cap = std::max<uint32_t>(c->resident_waves[G == 16][2], wgt::TW);
+    wgt::TransportParams PS{}, PO{};
+    uint32_t gs = 0, go = 0;
+    bool os = false, oo = false;
+    rc = plan_transport<WG_MODE_SEAL>(c, sb->desc, sb->n, sb->in, sb->in_size, sb->out, sb->out_size, nullptr,
+                                      sb->max_len, sb->flags, s, cap, G, c->lpt_hist, c->lpt_order, &PS, &gs, &os,
+                                      nullptr, true, false);
+    if (rc == WG_OK)
+      rc = plan_transport<WG_MODE_OPEN>(c, ob->desc, ob->n, ob->in, ob->in_size, ob->out, ob->out_size, ob->status,
+                                        ob->max_len, ob->flags & ~WG_F_AFTER_SEAL, s, cap, G, c->lpt_hist,
+                                        c->lpt_order, &PO, &go, &oo, nullptr, true, true);
+    if (rc == WG_OK && (gs != go || PS.slots != PO.slots || PS.order != PO.order))
+      rc = fail(WG_EINVAL, "k_step: seal and open plans differ (%u / %u workgroups)", gs, go);
+    if (rc == WG_OK) {
+      hipEvent_t ev;
+      record_start(c, s, &ev);
+      if (G == 16) hipLaunchKernelGGL(wgt::k_step<16>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+      else hipLaunchKernelGGL(wgt::k_step<8>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+      const hipError_t e = hipGetLastError();
+      record_end(c, s, ev);
+      if (e != hipSuccess) rc = fail(WG_EDEVICE, "k_step launch: %s", hipGetErrorString(e));
+    }
+  } else {
+    rc = launch_transport<WG_MODE_SEAL>(c, sb->desc, sb->n, sb->in, sb->in_size, sb->out, sb->out_size, nullptr,
+                                        sb->max_len, sb->flags, s, nullptr, &c->lpt_hist, &c->lpt_order);
+    if (rc == WG_OK)
+      rc = launch_transport<WG_MODE_OPEN>(c, ob->desc, ob->n, ob->in, ob->in_size, ob->out, ob->out_size, ob->status,
+                                          ob->max_len, ob->flags & ~WG_F_AFTER_SEAL, s, nullptr, &c->lpt_hist,
+                                          &c->lpt_order, same_plan);
+  }
   const int rr = ordered ? ws_release(c, s) : WG_OK;
   return rc != WG_OK ? rc : rr;
 }
@@ -449,15 +501,16 @@ const char* wg_version(void) { return "wgaead 0.2.0 gfx950"; }
 
 int wg_ctx_set_kernel(wg_ctx* c, const char* name, uint32_t lanes, uint32_t variant) {
   (void)lanes;
-  (void)variant;
   if (!c) return fail(WG_EINVAL, "ctx is NULL");
   int k;
   if (!name || !strcmp(name, "default") || !strcmp(name, "transport")) k = KERN_TRANSPORT;
   else if (!strcmp(name, "wave1")) k = KERN_WAVE1;
   else if (!strcmp(name, "tile")) k = KERN_TILE;
   else return fail(WG_EINVAL, "unknown transport kernel '%s'", name);
+  if (variant > 1u) return fail(WG_EINVAL, "unknown kernel variant %u", variant);
   std::lock_guard<std::mutex> lk(c->mu);
   c->kern = k;
+  c->step_two_launches = variant == 1u;
   return WG_OK;
 }
 
@@ -474,7 +527,7 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   c->key_slots = key_slots;
   c->ws_stream = (hipStream_t)-1;
   hipDeviceProp_t prop;
-  int bps = 0, bpo = 0;
+  int bl[2][3] = {{0, 0, 0}, {0, 0, 0}};  // workgroups per CU of each transport kernel
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->copy_out_stream, hipStreamNonBlocking) != hipSuccess ||
@@ -483,10 +536,16 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
       hipEventCreateWithFlags(&c->ev_kernel, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_ws, hipEventDisableTiming) != hipSuccess ||
       hipGetDeviceProperties(&prop, device) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&bps, wgt::k_transport<WG_MODE_SEAL>, 64 * wgt::TW, 0) !=
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&bl[0][0], wgt::k_transport<WG_MODE_SEAL, 8>, 64 * wgt::TW, 0) !=
           hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpo, wgt::k_transport<WG_MODE_OPEN>, 64 * wgt::TW, 0) !=
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&bl[0][1], wgt::k_transport<WG_MODE_OPEN, 8>, 64 * wgt::TW, 0) !=
           hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&bl[0][2], wgt::k_step<8>, 64 * wgt::TW, 0) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&bl[1][0], wgt::k_transport<WG_MODE_SEAL, 16>, 64 * wgt::TW, 0) !=
+          hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&bl[1][1], wgt::k_transport<WG_MODE_OPEN, 16>, 64 * wgt::TW, 0) !=
+          hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&bl[1][2], wgt::k_step<16>, 64 * wgt::TW, 0) != hipSuccess ||
       hipMalloc(&c->keys, (size_t)key_slots * 32) != hipSuccess ||
       // on the context's stream, like every later key write: a memset on the null stream can sit
       // behind another context's per-packet server in a shared hardware queue and land AFTER the
@@ -497,8 +556,10 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
     return fail(WG_ENOMEM, "context allocation failed on device %d", device);
   }
   c->keys_host.assign((size_t)key_slots * 32, 0);
-  c->resident_waves[0] = (uint32_t)std::max(bps, 1) * wgt::TW * (uint32_t)prop.multiProcessorCount;
-  c->resident_waves[1] = (uint32_t)std::max(bpo, 1) * wgt::TW * (uint32_t)prop.multiProcessorCount;
+  for (int w = 0; w < 2; ++w)
+    for (int k = 0; k < 3; ++k)
+      c->resident_waves[w][k] = (uint32_t)std::max(bl[w][k], 1) * wgt::TW * (uint32_t)prop.multiProcessorCount;
+  if (const char* e = getenv("WG_SLOT16")) c->slot16 = atoi(e);
   *out = c;
   return WG_OK;
 }
@@ -657,15 +718,15 @@ int wg_duplex_batch(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, void* str
         if (b->max_len > WG_MAX_PACKET) return fail(WG_E2BIG, "max_len %u > WG_MAX_PACKET", b->max_len);
       }
       // the two halves share the machine: each plans with half of the resident slots
-      const uint64_t cap = 4ull * std::max<uint32_t>(std::min(c->resident_waves[0], c->resident_waves[1]), wgt::TW);
+      const uint64_t cap = std::max<uint32_t>(std::min(c->resident_waves[0][0], c->resident_waves[0][1]) / 2u, wgt::TW);
       wgt::TransportParams PS{}, PO{};
       uint32_t gs = 0, go = 0;
       bool os = false, oo = false;
       int rc = plan_transport<WG_MODE_SEAL>(c, sb->desc, sb->n, sb->in, sb->in_size, sb->out, sb->out_size, nullptr,
-                                            sb->max_len, sb->flags, s, cap, c->lpt_hist, c->lpt_order, &PS, &gs, &os);
+                                            sb->max_len, sb->flags, s, cap, 8u, c->lpt_hist, c->lpt_order, &PS, &gs, &os);
       if (rc != WG_OK) return rc;
       rc = plan_transport<WG_MODE_OPEN>(c, ob->desc, ob->n, ob->in, ob->in_size, ob->out, ob->out_size, ob->status,
-                                        ob->max_len, ob->flags, s, cap, c->lpt_hist2, c->lpt_order2, &PO, &go, &oo);
+                                        ob->max_len, ob->flags, s, cap, 8u, c->lpt_hist2, c->lpt_order2, &PO, &go, &oo);
       if (rc != WG_OK) return rc;
       hipEvent_t ev;
       record_start(c, s, &ev);

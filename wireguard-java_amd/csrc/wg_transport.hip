@@ -109,7 +109,7 @@ struct TransportParams {
   const wg_pkt* desc;
   const uint32_t* order;  // batch position -> packet index (longest first); nullptr = identity
   uint32_t n;
-  uint32_t slots;         // S = 8 x waves in the grid
+  uint32_t slots;         // S = (64 / G) x waves in the grid
   uint32_t max_len;
   uint32_t key_slots;
   const uint8_t* in;
@@ -150,22 +150,26 @@ struct TransportParams {
 #define WG_PH_STORE(idx) do {} while (0)
 #endif
 
-// ---- lane exchange inside an 8-lane slot -------------------------------------------
+// ---- lane exchange inside a slot of G lanes (G = 8 or 16) ---------------------------
 // ds_swizzle bitmask mode inside each 32-lane half: src = ((lane & and) | or) ^ xor.
-template <int K>
-__device__ __forceinline__ uint32_t bcast8(uint32_t v) {  // every lane of the slot reads lane K of it
-  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (K << 5));
+template <int G, int K>
+__device__ __forceinline__ uint32_t bcastg(uint32_t v) {  // every lane of the slot reads lane K of it
+  static_assert(G == 8 || G == 16, "slots of 8 or 16 lanes");
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (0x20 - G) | (K << 5));
 }
+template <int K>
+__device__ __forceinline__ uint32_t bcast8(uint32_t v) { return bcastg<8, K>(v); }
 template <int X>
-__device__ __forceinline__ uint32_t xor8(uint32_t v) {  // lane reads lane ^ X (X < 8)
+__device__ __forceinline__ uint32_t xorg(uint32_t v) {  // lane reads lane ^ X (X < 16)
   return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1f | (X << 10));
 }
 
 // The same exchanges through DPP (VALU, no LDS round trip) for the dependent chains of the
-// r-power scan and the slot sum: row_shr:K (lane j reads j - K; lanes j < K of a slot get
-// garbage and must not use it), lane ^ 1, lane ^ 2 (quad_perm) and lane ^ 4 (two half moves).
+// r-power scan and the slot sum: row_shr:K (lane j reads j - K inside its 16-lane row; lanes j < K
+// of a slot get garbage and must not use it), lane ^ 1, lane ^ 2 (quad_perm), lane ^ 4 (two half
+// moves) and lane ^ 8 (row_ror:8, 16-lane slots).
 template <int K>
-__device__ __forceinline__ uint32_t shr8_dpp(uint32_t v) {
+__device__ __forceinline__ uint32_t shr_dpp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 | K, 0xf, 0xf, false);
 }
 __device__ __forceinline__ uint32_t xor1_dpp(uint32_t v) {
@@ -178,6 +182,9 @@ __device__ __forceinline__ uint32_t xor4_dpp(uint32_t v) {
   // lanes 4-7 of a slot (banks 1, 3) read j - 4 (row_shr:4), lanes 0-3 (banks 0, 2) read j + 4 (row_shl:4)
   const int t = __builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xa, false);
   return (uint32_t)__builtin_amdgcn_update_dpp(t, (int)v, 0x104, 0xf, 0x5, false);
+}
+__device__ __forceinline__ uint32_t xor8_dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
 }
 
 // ---- validity of one transport descriptor (shared by seal, open and the framing) ----
@@ -289,15 +296,21 @@ __device__ __forceinline__ uint32_t opaque_lane() {
   return x;
 }
 
-// The per-wave body of k_transport (and of each half of k_duplex): workgroup `blk` of the
-// direction's grid; img / rec are this wave's 4-KB image and slot records in LDS.
-template <int MODE>
+// The per-wave body of k_transport (and of each half of k_duplex / k_step): workgroup `blk` of the
+// direction's grid; img / rec are this wave's 4-KB image and slot records in LDS. G = lanes per
+// slot: 8 (8 slots per wave, rounds of 8 blocks) or 16 (4 slots, rounds of 16 blocks = 1 KB:
+// long packets take half as many rounds, so a mixed-length batch can pair them longest-first at
+// 8 waves per SIMD).
+template <int MODE, int G = 8>
 __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_t blk, uint32_t wv, uint4* const img,
                                                SlotRec* const rec) {
   static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
+  static_assert(G == 8 || G == 16, "slots of 8 or 16 lanes");
+  constexpr uint32_t SH = G == 8 ? 3u : 4u;  // log2 G
+  constexpr uint32_t JM = G - 1u;
   if (P.prio_step) __builtin_amdgcn_s_setprio(3);  // first instruction: a fresh wave is never starved
   const uint32_t S = P.slots;
-  const uint32_t g = (blk * TW + wv) * 8u + (opaque_lane() >> 3);
+  const uint32_t g = (blk * TW + wv) * (64u / G) + (opaque_lane() >> SH);
 
   // descriptor prefetch: dword j of the next packet's wg_pkt (32 B = 8 dwords, one per lane)
   uint32_t gen = 0;
@@ -336,14 +349,15 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
     }
     // ---- slots without a packet take their next one ------------------------------------
     if (!have && nxt != ~0u) {
-      const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
+      const uint32_t lane = opaque_lane(), s = lane >> SH, j = lane & JM;
       pkt = nxt;
 #ifdef WG_DIAG
       { uint32_t dn = dnext; asm volatile("s_waitcnt vmcnt(0)" : "+v"(dn)); dnext = dn; }
       WG_PH(6);
 #endif
-      const uint32_t d0 = bcast8<0>(dnext), d1 = bcast8<1>(dnext), d2 = bcast8<2>(dnext), d3 = bcast8<3>(dnext);
-      const uint32_t len = bcast8<6>(dnext), ks = bcast8<7>(dnext);
+      const uint32_t d0 = bcastg<G, 0>(dnext), d1 = bcastg<G, 1>(dnext), d2 = bcastg<G, 2>(dnext),
+                     d3 = bcastg<G, 3>(dnext);
+      const uint32_t len = bcastg<G, 6>(dnext), ks = bcastg<G, 7>(dnext);
       const uint64_t in_off = (uint64_t)d0 | ((uint64_t)d1 << 32);
       const uint64_t out_off = (uint64_t)d2 | ((uint64_t)d3 << 32);
       const bool valid =
@@ -368,11 +382,11 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         uint32_t v = k[0];
 #pragma unroll
         for (uint32_t i = 1; i < 8u; ++i) v = j == i ? k[i] : v;
-        if (valid) ((uint32_t*)rec[s].key)[j] = v;
-      } else if (valid) {
+        if (valid && j < 8u) ((uint32_t*)rec[s].key)[j] = v;
+      } else if (valid && j < 8u) {
         ((uint32_t*)rec[s].key)[j] = P.keys[8u * ks + j];
       }
-      const uint32_t c0 = bcast8<4>(dnext), c1 = bcast8<5>(dnext);  // all 8 lanes active: swizzles read live lanes
+      const uint32_t c0 = bcastg<G, 4>(dnext), c1 = bcastg<G, 5>(dnext);  // all lanes active: swizzles read live lanes
       if (j == 0) {
         rec[s].addr = make_uint4(d0, d1, d2, d3);
         rec[s].meta = make_uint4(c0, c1, len, (valid ? 1u : 0u) | al);
@@ -383,22 +397,22 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
       ++gen;
       const uint32_t pos = batch_pos(g, gen, S);
       nxt = pos < P.n ? (P.order ? P.order[pos] : pos) : ~0u;
-      dnext = nxt != ~0u ? ((const uint32_t*)(P.desc + nxt))[j] : 0u;
+      dnext = nxt != ~0u ? ((const uint32_t*)(P.desc + nxt))[j & 7u] : 0u;
     }
     if (!__any(have)) break;
     wave_lds_sync();  // the slot records before the lanes read them
     WG_PH(0);
 
     // this round's packet parameters, read once (meta = {ctr lo, ctr hi, len, flags})
-    const uint4 meta = rec[opaque_lane() >> 3].meta;
+    const uint4 meta = rec[opaque_lane() >> SH].meta;
     const uint32_t len = meta.z;
     const uint32_t nb = (meta.w & 1u) ? ((len + 63u) >> 6) + 1u : 0u;
     uint32_t x[16];
     {
       // ---- payload prefetch: LDS-DMA straight into this lane's slice of the image ---------
       // (no registers held across the ARX rounds)
-      const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
-      const uint32_t b = 8u * round + j;
+      const uint32_t lane = opaque_lane(), s = lane >> SH, j = lane & JM;
+      const uint32_t b = G * round + j;
 #ifdef WG_ABL_NODMA
       if (false) {
 #else
@@ -440,17 +454,17 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         }
       }
       {
-        const uint32_t H[12] = {bcast8<1>(hc[0]), bcast8<1>(hc[1]), bcast8<1>(hc[2]), bcast8<1>(hc[3]),
-                                bcast8<2>(hc[0]), bcast8<2>(hc[1]), bcast8<2>(hc[2]), bcast8<2>(hc[3]),
-                                bcast8<3>(hc[0]), bcast8<3>(hc[1]), bcast8<3>(hc[2]), bcast8<3>(hc[3])};
+        const uint32_t H[12] = {bcastg<G, 1>(hc[0]), bcastg<G, 1>(hc[1]), bcastg<G, 1>(hc[2]), bcastg<G, 1>(hc[3]),
+                                bcastg<G, 2>(hc[0]), bcastg<G, 2>(hc[1]), bcastg<G, 2>(hc[2]), bcastg<G, 2>(hc[3]),
+                                bcastg<G, 3>(hc[0]), bcastg<G, 3>(hc[1]), bcastg<G, 3>(hc[2]), bcastg<G, 3>(hc[3])};
         chacha20_block_hoisted(rec[s].key, b, meta.x, meta.y, 0u, H, x);
       }
 #endif
     }
 
     if (__any(have && round == 0)) {  // round 0: lane 0 of the slot holds the one-time key r || s
-      const uint32_t lane = opaque_lane(), s = lane >> 3;
-      if (have && round == 0 && (lane & 7u) == 0) {
+      const uint32_t lane = opaque_lane(), s = lane >> SH;
+      if (have && round == 0 && (lane & JM) == 0) {
         rec[s].R0 = make_uint4(x[0], x[1], x[2], x[3]);  // raw r, replaced by R = r^8 below
         rec[s].s = make_uint4(x[4], x[5], x[6], x[7]);
       }
@@ -459,8 +473,8 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
     WG_PH(1);
     // ---- XOR, store, MAC input into the image, one 16-B chunk at a time ----------------------
     {
-      const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
-      const uint32_t b = 8u * round + j;
+      const uint32_t lane = opaque_lane(), s = lane >> SH, j = lane & JM;
+      const uint32_t b = G * round + j;
       if (have && b < nb && b > 0u) {
         const uint32_t off = 64u * (b - 1u);
         const uint32_t nbytes = min(64u, len - off);
@@ -496,40 +510,41 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
     // the length block le64(0) || le64(len) is MAC chunk nc (the first after the data): the lane
     // whose counter block holds it writes it into the image, so the Horner steps read it like data
     {
-      const uint32_t lane = opaque_lane(), j = lane & 7u;
+      const uint32_t lane = opaque_lane(), j = lane & JM;
       const uint32_t nc = (len + 15u) >> 4;
-      if (have && (meta.w & 1u) && 8u * round + j == (nc >> 2) + 1u) {
+      if (have && (meta.w & 1u) && G * round + j == (nc >> 2) + 1u) {
         img[64u * (nc & 3u) + lane] = make_uint4(0u, 0u, len, 0u);
       }
     }
     wave_lds_sync();
     WG_PH(2);
 
-    // ---- round 0: r^1..r^8 (lane j gets r^(j+1)), R = r^8, W = r^(8-j) --------------------
+    // ---- round 0: r^1..r^G (lane j gets r^(j+1)), R = r^G, W = r^(G-j) --------------------
     // (after the XOR phase, so the 32 registers of keystream and payload are free again)
     if (__any(have && round == 0)) {
       if (have && round == 0) {
-        const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
+        const uint32_t lane = opaque_lane(), s = lane >> SH, j = lane & JM;
         const uint4 rr = rec[s].R0;
         uint32_t y[5];
         poly_r_limbs(rr.x, rr.y, rr.z, rr.w, y);
 #ifndef WG_ABL_NOSCAN
 #pragma unroll
-        for (uint32_t st = 1; st < 8u; st <<= 1) {
+        for (uint32_t st = 1; st < G; st <<= 1) {
 #else
-        for (uint32_t st = 8; st < 8u; st <<= 1) {
+        for (uint32_t st = G; st < G; st <<= 1) {
 #endif
           uint32_t z[5], zs[5];
 #pragma unroll
-          for (int i = 0; i < 5; ++i) z[i] = st == 1 ? shr8_dpp<1>(y[i]) : st == 2 ? shr8_dpp<2>(y[i]) : shr8_dpp<4>(y[i]);
+          for (int i = 0; i < 5; ++i)
+            z[i] = st == 1 ? shr_dpp<1>(y[i]) : st == 2 ? shr_dpp<2>(y[i]) : st == 4 ? shr_dpp<4>(y[i]) : shr_dpp<8>(y[i]);
           poly_scale5(z, zs);
           if (j >= st) poly_mul(y, z, zs);
         }
         uint32_t R[5];
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
-          R[i] = bcast8<7>(y[i]);
-          W[i] = xor8<7>(y[i]);
+          R[i] = bcastg<G, G - 1>(y[i]);
+          W[i] = xorg<G - 1>(y[i]);
           acc[i] = 0;
         }
         if (j == 0) {
@@ -548,25 +563,25 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
 #else
     if (have && (meta.w & 1u)) {
 #endif
-      const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
+      const uint32_t lane = opaque_lane(), s = lane >> SH, j = lane & JM;
       {
         const uint32_t nc = (len + 15u) >> 4;
-        const uint32_t M = nc + 1u, D = 8u * ((M + 7u) >> 3) - M;
-        const uint32_t c_lo = round ? 32u * round - 4u : 0u;
+        const uint32_t M = nc + 1u, D = G * ((M + JM) >> SH) - M;
+        const uint32_t c_lo = round ? 4u * G * round - 4u : 0u;
         // chunk nc (after the data) is the length block le64(0) || le64(len): taken here when it
         // falls inside this round's window, at the finish otherwise
-        const uint32_t c_end = min(nc + 1u, 32u * round + 28u);
-        const uint32_t c0 = c_lo + ((j - ((c_lo + D) & 7u)) & 7u);
-        // chunk ci of the round sits in lane (ci >> 2) + 1 - 8 round of the slot, row ci & 3
-        const uint4* ip = &img[64u * (c0 & 3u) + (lane & ~7u) + ((c0 + 4u) >> 2) - 8u * round];
+        const uint32_t c_end = min(nc + 1u, 4u * G * round + 4u * G - 4u);
+        const uint32_t c0 = c_lo + ((j - ((c_lo + D) & JM)) & JM);
+        // chunk ci of the round sits in lane (ci >> 2) + 1 - G round of the slot, row ci & 3
+        const uint4* ip = &img[64u * (c0 & 3u) + (lane & ~JM) + ((c0 + 4u) >> 2) - G * round];
         const uint4 q0 = rec[s].R0, q1 = rec[s].R1, q2 = rec[s].R2;
         const uint32_t R[5] = {q0.x, q0.y, q0.z, q0.w, q1.x};
         const uint32_t Rs[5] = {0u, q1.y, q1.z, q1.w, q2.x};
 #pragma unroll
         for (uint32_t t = 0; t < 4u; ++t) {
-          if (c0 + 8u * t < c_end) {
+          if (c0 + G * t < c_end) {
 #ifndef WG_ABL_NOPOLYLDS
-            uint4 v = ip[2u * t];
+            uint4 v = ip[(G / 4u) * t];
 #else
             uint4 v = make_uint4(acc[0] ^ t, acc[1], acc[2] + c0, acc[3]);
 #endif
@@ -583,13 +598,13 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
 
     WG_PH(4);
     // ---- finish the packets whose last round this was ---------------------------------------
-    const bool done = have && 8u * (round + 1u) >= nb;  // invalid packets (nb = 0) finish at once
+    const bool done = have && G * (round + 1u) >= nb;  // invalid packets (nb = 0) finish at once
     if (__any(done)) {
       if (done) {  // slot-uniform: every lane of a finishing slot is here
-        const uint32_t lane = opaque_lane(), s = lane >> 3, j = lane & 7u;
+        const uint32_t lane = opaque_lane(), s = lane >> SH, j = lane & JM;
         const bool valid = meta.w & 1u;
         if (valid) {
-          if (j == 7u && ((len + 15u) >> 4) >= 32u * round + 28u) {  // length block not taken in the loop
+          if (j == JM && ((len + 15u) >> 4) >= 4u * G * round + 4u * G - 4u) {  // length block not taken in the loop
             const uint4 q0 = rec[s].R0, q1 = rec[s].R1, q2 = rec[s].R2;
             const uint32_t R[5] = {q0.x, q0.y, q0.z, q0.w, q1.x};
             const uint32_t Rs[5] = {0u, q1.y, q1.z, q1.w, q2.x};
@@ -609,6 +624,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
           acc[i] += xor1_dpp(acc[i]);
           acc[i] += xor2_dpp(acc[i]);
           acc[i] += xor4_dpp(acc[i]);
+          if constexpr (G == 16) acc[i] += xor8_dpp(acc[i]);
         }
         const uint4 ad = rec[s].addr;
         const uint8_t* inp = P.in + ((uint64_t)ad.x | ((uint64_t)ad.y << 32));
@@ -639,7 +655,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
           }
         }
         if constexpr (MODE == WG_MODE_OPEN) {
-          bad = bcast8<0>(bad);
+          bad = bcastg<G, 0>(bad);
           if (j == 0 && P.status) {
             uint32_t st = bad ? WG_PKT_BADTAG : WG_PKT_OK;
             if (!bad && P.rx) {  // fused receive-side check on the plaintext this slot wrote
@@ -649,7 +665,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
             P.status[pkt] = st;
           }
           if (bad && valid) {  // scrub the unauthenticated plaintext written by this launch
-            for (uint32_t i = j; i < len; i += 8u) outp[i] = 0;
+            for (uint32_t i = j; i < len; i += G) outp[i] = 0;
           }
         }
         have = false;
@@ -662,12 +678,12 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
   WG_PH_STORE(blk * TW + wv);
 }
 
-template <int MODE>
+template <int MODE, int G = 8>
 __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8))) k_transport(TransportParams P) {
   __shared__ uint4 img_[TW][4 * 64];  // 4 KB per wave: [chunk q][lane] = the round's payload / MAC input
   __shared__ SlotRec rec_[TW][8];     // 1 KB per wave
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  transport_body<MODE>(P, blockIdx.x, wv, img_[wv], rec_[wv]);
+  transport_body<MODE, G>(P, blockIdx.x, wv, img_[wv], rec_[wv]);
 }
 
 // One launch, two directions (wg_duplex_batch): a node's outgoing batch sealed and its
@@ -693,6 +709,25 @@ k_duplex(TransportParams S, TransportParams O, uint32_t seal_blocks, uint32_t op
   }
   if (seal) transport_body<WG_MODE_SEAL>(S, idx, wv, img_[wv], rec_[wv]);
   else transport_body<WG_MODE_OPEN>(O, idx, wv, img_[wv], rec_[wv]);
+}
+
+// One launch, one dependent step (wg_duplex_batch with WG_F_AFTER_SEAL): every wave seals its
+// packets and then opens the same batch positions of the open batch, which read what its own
+// seal wrote (open packet i is ordered after seal packet i, include/wgaead.h). Both halves use one
+// grid and one packet order, so slot g opens exactly the packets it sealed. The waves that finish
+// sealing first start opening while the others still seal: the seal launch's tail and the open
+// launch's start, which two back-to-back launches leave partly idle, overlap.
+template <int G = 8>
+__global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)))
+k_step(TransportParams S, TransportParams O) {
+  __shared__ uint4 img_[TW][4 * 64];
+  __shared__ SlotRec rec_[TW][8];
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  transport_body<WG_MODE_SEAL, G>(S, blockIdx.x, wv, img_[wv], rec_[wv]);
+  // the open reads the ciphertext and tags this wave just stored: wait until the stores are
+  // performed and drop this CU's L1 lines (an in-place seal read the plaintext through them)
+  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
+  transport_body<WG_MODE_OPEN, G>(O, blockIdx.x, wv, img_[wv], rec_[wv]);
 }
 
 // ---- longest-first order for mixed-length batches (LPT) ----------------------------------
