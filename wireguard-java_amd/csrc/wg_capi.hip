@@ -96,7 +96,9 @@ struct wg_ctx {
   // waves resident at once (occupancy) of k_transport<SEAL>, <OPEN> and k_step, with 8-lane [0] and
   // 16-lane [1] slots
   uint32_t resident_waves[2][3] = {{0, 0, 0}, {0, 0, 0}};
-  int slot16 = 1;                         // 16-lane slots for mixed-length batches (WG_SLOT16=0: never)
+  int slot16 = 0;                         // 16-lane slots for mixed-length batches (WG_SLOT16=1, A/B)
+  int prio_mode = -1;                     // progress-based issue priority: -1 mixed batches only, 0 off, 1 on (WG_PRIO)
+  uint32_t prio_levels = 4;               // priority levels the schedule steps through (WG_PRIO_LEVELS, 1..4)
   bool step_two_launches = false;         // wg_ctx_set_kernel variant 1: WG_F_AFTER_SEAL as seal + open launches
   // plan workspace: k_tile block scan, k_transport longest-first order
   DevBuf plan_nb, plan_prefix, plan_tiles, plan_ntiles, plan_tmp, lpt_hist, lpt_order;
@@ -331,7 +333,11 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   // so the waves that have done the least work issue first (C2 +2%); uniform batches keep the
   // default oldest-first arbitration (the same schedule cost C1 2%)
   const uint32_t max_rounds = (host_pkt_blocks<WG_MODE_SEAL>(max_len) + G - 1u) / G;
-  P.prio_step = (flags & WG_F_UNIFORM) ? 0u : std::max<uint32_t>(1u, (uint32_t)((per_slot * max_rounds + 3u) / 4u));
+  const uint32_t lv = c->prio_levels;
+  const uint32_t pstep = std::max<uint32_t>(1u, (uint32_t)((per_slot * max_rounds + lv - 1u) / lv));
+  P.prio_step = (flags & WG_F_UNIFORM) ? 0u : pstep;
+  if (c->prio_mode == 0) P.prio_step = 0;  // WG_PRIO=0 / 1: issue priority off / on for every batch (A/B)
+  else if (c->prio_mode == 1) P.prio_step = pstep;
   if (!(flags & WG_F_UNIFORM) && per_slot > 1) {  // longest-first order (LPT) for the snake
     // reuse_order: the order already in lpt_order (the seal of the same packets, WG_F_AFTER_SEAL);
     // private_ws: buffers owned by the caller's stream (no shared-workspace ordering)
@@ -459,8 +465,13 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
       rc = plan_transport<WG_MODE_OPEN>(c, ob->desc, ob->n, ob->in, ob->in_size, ob->out, ob->out_size, ob->status,
                                         ob->max_len, ob->flags & ~WG_F_AFTER_SEAL, s, cap, G, c->lpt_hist,
                                         c->lpt_order, &PO, &go, &oo, nullptr, true, true);
+    // one issue-priority schedule over the seal and open halves (the rounds of both)
+    if (PS.prio_step) PS.prio_step = PO.prio_step = 2u * PS.prio_step;
     if (rc == WG_OK && (gs != go || PS.slots != PO.slots || PS.order != PO.order))
       rc = fail(WG_EINVAL, "k_step: seal and open plans differ (%u / %u workgroups)", gs, go);
+#ifdef WG_DIAG
+    if (PO.stamps) PO.stamps += 10ull * gs * wgt::TW;  // the open half's stamps after the seal half's
+#endif
     if (rc == WG_OK) {
       hipEvent_t ev;
       record_start(c, s, &ev);
@@ -560,6 +571,8 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
     for (int k = 0; k < 3; ++k)
       c->resident_waves[w][k] = (uint32_t)std::max(bl[w][k], 1) * wgt::TW * (uint32_t)prop.multiProcessorCount;
   if (const char* e = getenv("WG_SLOT16")) c->slot16 = atoi(e);
+  if (const char* e = getenv("WG_PRIO")) c->prio_mode = atoi(e);
+  if (const char* e = getenv("WG_PRIO_LEVELS")) c->prio_levels = (uint32_t)std::min(4, std::max(1, atoi(e)));
   *out = c;
   return WG_OK;
 }

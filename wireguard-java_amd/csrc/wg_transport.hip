@@ -301,14 +301,16 @@ __device__ __forceinline__ uint32_t opaque_lane() {
 // slot: 8 (8 slots per wave, rounds of 8 blocks) or 16 (4 slots, rounds of 16 blocks = 1 KB:
 // long packets take half as many rounds, so a mixed-length batch can pair them longest-first at
 // 8 waves per SIMD).
+// iter: rounds this wave has run so far in the launch (the issue-priority schedule spans both
+// halves of a k_step launch).
 template <int MODE, int G = 8>
 __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_t blk, uint32_t wv, uint4* const img,
-                                               SlotRec* const rec) {
+                                               SlotRec* const rec, uint32_t& iter) {
   static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
   static_assert(G == 8 || G == 16, "slots of 8 or 16 lanes");
   constexpr uint32_t SH = G == 8 ? 3u : 4u;  // log2 G
   constexpr uint32_t JM = G - 1u;
-  if (P.prio_step) __builtin_amdgcn_s_setprio(3);  // first instruction: a fresh wave is never starved
+  if (P.prio_step && iter == 0) __builtin_amdgcn_s_setprio(3);  // first instruction: a fresh wave is never starved
   const uint32_t S = P.slots;
   const uint32_t g = (blk * TW + wv) * (64u / G) + (opaque_lane() >> SH);
 
@@ -335,7 +337,6 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
   // waves runs ahead and the waves finish one after another. A wave drops one priority level
   // every prio_step rounds instead, so the waves that have done the least work issue first
   // (C2 +2%, C1 -2%: DESIGN.md §4.2).
-  uint32_t iter = 0;  // wave-uniform
   WG_PH_DECL
   while (true) {
     if (P.prio_step) {
@@ -683,7 +684,8 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
   __shared__ uint4 img_[TW][4 * 64];  // 4 KB per wave: [chunk q][lane] = the round's payload / MAC input
   __shared__ SlotRec rec_[TW][8];     // 1 KB per wave
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  transport_body<MODE, G>(P, blockIdx.x, wv, img_[wv], rec_[wv]);
+  uint32_t iter = 0;
+  transport_body<MODE, G>(P, blockIdx.x, wv, img_[wv], rec_[wv], iter);
 }
 
 // One launch, two directions (wg_duplex_batch): a node's outgoing batch sealed and its
@@ -707,8 +709,9 @@ k_duplex(TransportParams S, TransportParams O, uint32_t seal_blocks, uint32_t op
     seal = seal_blocks > open_blocks;
     idx = b - m;
   }
-  if (seal) transport_body<WG_MODE_SEAL>(S, idx, wv, img_[wv], rec_[wv]);
-  else transport_body<WG_MODE_OPEN>(O, idx, wv, img_[wv], rec_[wv]);
+  uint32_t iter = 0;
+  if (seal) transport_body<WG_MODE_SEAL>(S, idx, wv, img_[wv], rec_[wv], iter);
+  else transport_body<WG_MODE_OPEN>(O, idx, wv, img_[wv], rec_[wv], iter);
 }
 
 // One launch, one dependent step (wg_duplex_batch with WG_F_AFTER_SEAL): every wave seals its
@@ -723,11 +726,12 @@ k_step(TransportParams S, TransportParams O) {
   __shared__ uint4 img_[TW][4 * 64];
   __shared__ SlotRec rec_[TW][8];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  transport_body<WG_MODE_SEAL, G>(S, blockIdx.x, wv, img_[wv], rec_[wv]);
+  uint32_t iter = 0;  // one issue-priority schedule over both halves (plan_transport: prio_step of the step)
+  transport_body<WG_MODE_SEAL, G>(S, blockIdx.x, wv, img_[wv], rec_[wv], iter);
   // the open reads the ciphertext and tags this wave just stored: wait until the stores are
   // performed and drop this CU's L1 lines (an in-place seal read the plaintext through them)
   asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
-  transport_body<WG_MODE_OPEN, G>(O, blockIdx.x, wv, img_[wv], rec_[wv]);
+  transport_body<WG_MODE_OPEN, G>(O, blockIdx.x, wv, img_[wv], rec_[wv], iter);
 }
 
 // ---- longest-first order for mixed-length batches (LPT) ----------------------------------
