@@ -437,6 +437,7 @@ def main():
     ev0.record()
     for _ in range(args.steps):
         step()
+    t_enq = time.perf_counter()  # host time to enqueue the steps (the GPU idles if it is ~ ms_per_step)
     ev1.record()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -522,6 +523,7 @@ def main():
             "ramp_ms": args.ramp_ms,
             "ramp_steps": ramp_steps,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "host_enqueue_ms_per_step": round((t_enq - t0) * 1e3 / args.steps, 4),
             "higher_is_better": True,
             "scaling": "strong" if args.workload == "c3" else "weak",
             "vs_baseline": None,

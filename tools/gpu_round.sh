@@ -27,6 +27,8 @@ timeout -k 10 400 python bench.py > $O/bench_c1.json 2> $O/bench.err || die benc
 cat $O/bench_c1.json
 step "bench c1 (serial)"
 timeout -k 10 300 python bench.py --mode serial --no-cpu-baseline > $O/bench_c1_serial.json 2>> $O/bench.err || die bench_c1_serial $?
+step "bench c1 (step as two launches)"
+timeout -k 10 300 python bench.py --variant 1 --no-cpu-baseline > $O/bench_c1_step2.json 2>> $O/bench.err || die bench_c1_step2 $?
 step "bench c2"
 timeout -k 10 300 python bench.py --workload c2 > $O/bench_c2.json 2>> $O/bench.err || die bench_c2 $?
 cat $O/bench_c2.json
