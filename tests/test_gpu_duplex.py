@@ -161,10 +161,13 @@ def _after_seal(engine, n, lengths, nkeys, uniform, forge=()):
         assert np.array_equal(back[o:o + L], pt[o:o + L]), f"plaintext of packet {i}"
 
 
-def test_after_seal_c1_shaped():
+@pytest.mark.parametrize("variant", [0, 1])
+def test_after_seal_c1_shaped(variant):
+    """variant 0: one k_step launch; 1: the same step as a seal launch and an open launch."""
     W = wg()
     eng = W.Engine(0, key_slots=1)
     try:
+        eng.set_kernel("default", variant=variant)
         _after_seal(eng, 65536, np.full(65536, 1420, np.int64), 1, uniform=True)
     finally:
         eng.close()
@@ -181,9 +184,12 @@ def test_after_seal_ragged_sizes(n, L):
 
 
 @pytest.mark.parametrize("n", [3000, 40000])
-def test_after_seal_mixed_lengths(n):
+@pytest.mark.parametrize("slot16", ["0", "1"])
+def test_after_seal_mixed_lengths(n, slot16, monkeypatch):
     """Mixed lengths: 40000 packets take two per slot, so the batch is ordered longest-first once
-    and the open reuses the seal's order."""
+    and the open reuses the seal's order. slot16 "1": 16-lane slots (WG_SLOT16, read when the
+    context is created)."""
+    monkeypatch.setenv("WG_SLOT16", slot16)
     W = wg()
     eng = W.Engine(0, key_slots=16)
     try:

@@ -389,6 +389,22 @@ def test_randomized_batches_vs_oracle(engine, torch_dev, it):
     tags. Seal output must equal the oracle's for the valid packets and leave the rest
     untouched; open must report exactly the invalid and forged packets and zero-fill only
     the forged packets' plaintexts."""
+    _randomized_batch(engine, torch_dev, it)
+
+
+@pytest.mark.parametrize("it", [1, 2, 4, 5])
+def test_randomized_batches_16_lane_slots(torch_dev, it, monkeypatch):
+    """The same random mixed-length batches with 16-lane slots (WG_SLOT16=1: rounds of 16 blocks,
+    4 slots per wave, 4-step r-power scan, 4-step slot sum)."""
+    monkeypatch.setenv("WG_SLOT16", "1")
+    eng = wg().Engine(0, key_slots=4096)
+    try:
+        _randomized_batch(eng, torch_dev, it)
+    finally:
+        eng.close()
+
+
+def _randomized_batch(engine, torch_dev, it):
     rng = np.random.default_rng(1000 + it)
     n = int(rng.integers(1, 2500))
     if it % 3 == 0:
