@@ -68,21 +68,25 @@ def splitmix_np(seed: int, n: int) -> np.ndarray:
     return z.astype("<u8").view(np.uint8)[:n].copy()
 
 
-def build_workload(name: str, rank: int, world: int):
-    """Per-rank packet batch: (lengths, key_slot per packet, counters, nkeys, description)."""
+def build_workload(name: str, rank: int, world: int, packets: int = 0, keys: int = 0):
+    """Per-rank packet batch: (lengths, key_slot per packet, counters, nkeys, description).
+    packets / keys (diagnostic runs only, --packets / --keys): another batch size or session count
+    for C1 / C2; the description then says so."""
     seed = 0x5EED2026 + 7919 * rank
     if name == "c1":
-        n, L = 65536, 1420
+        n, L, k = packets or 65536, 1420, keys or 1
         lengths = np.full(n, L, np.int64)
-        slots = np.zeros(n, np.int64)
-        counters = np.arange(n, dtype=np.uint64)
-        return lengths, slots, counters, 1, f"C1: {n} x {L}B per GPU, one session key per GPU", True
+        slots = np.arange(n, dtype=np.int64) % k
+        counters = np.arange(n, dtype=np.uint64) // k
+        tag = "" if (n, k) == (65536, 1) else f" [diagnostic: {n} packets, {k} keys]"
+        return lengths, slots, counters, k, f"C1: {n} x {L}B per GPU, one session key per GPU{tag}", True
     if name == "c2":
-        n = 65536
+        n, k = packets or 65536, keys or 256
         lengths = (64 + splitmix_np(seed, 4 * n).view("<u4") % (9000 - 64 + 1)).astype(np.int64)
-        slots = np.arange(n, dtype=np.int64) % 256
-        counters = (np.arange(n, dtype=np.uint64) // 256)
-        return lengths, slots, counters, 256, f"C2: {n} packets per GPU, 64..9000B, 256 session keys", False
+        slots = np.arange(n, dtype=np.int64) % k
+        counters = (np.arange(n, dtype=np.uint64) // k)
+        tag = "" if (n, k) == (65536, 256) else f" [diagnostic: {n} packets, {k} keys]"
+        return lengths, slots, counters, k, f"C2: {n} packets per GPU, 64..9000B, 256 session keys{tag}", False
     if name == "c3":
         total, L, sessions = 8 * 1024 * 1024, 1420, 1024
         # session s -> GPU s mod world; each session's packets carry its own counters
@@ -323,6 +327,9 @@ def main():
     # --variant 1: a WG_F_AFTER_SEAL step as two launches (seal, then open) instead of one k_step launch
     ap.add_argument("--variant", type=int, default=0, choices=[0, 1])
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
+    # diagnostic knobs (not the metric's configuration): batch size and session count of C1 / C2
+    ap.add_argument("--packets", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--keys", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
@@ -346,7 +353,7 @@ def main():
     torch.cuda.set_device(dev)
 
     wg = importlib.import_module("wireguard-java_amd")
-    lengths, slots, counters, nkeys, wdesc, uniform = build_workload(args.workload, rank, world)
+    lengths, slots, counters, nkeys, wdesc, uniform = build_workload(args.workload, rank, world, args.packets, args.keys)
     n = len(lengths)
     keys = splitmix_np(0xC0FFEE + rank, 32 * nkeys)
     eng = wg.Engine(local, key_slots=max(nkeys, 1))

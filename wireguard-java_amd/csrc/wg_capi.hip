@@ -99,10 +99,14 @@ struct wg_ctx {
   int slot16 = 0;                         // 16-lane slots for mixed-length batches (WG_SLOT16=1, A/B)
   int prio_mode = -1;                     // progress-based issue priority: -1 mixed batches only, 0 off, 1 on (WG_PRIO)
   uint32_t prio_levels = 4;               // priority levels the schedule steps through (WG_PRIO_LEVELS, 1..4)
+  uint32_t mixed_per_slot = 0;            // packets per slot for mixed batches (0: planned; WG_MIXED_PER_SLOT, A/B)
+  uint32_t mixed_split = 0;               // > 0: mixed batches one packet per slot, packets of more than this
+                                          // many 8-block rounds in 16-lane slots (WG_MIXED_SPLIT)
   bool step_two_launches = false;         // wg_ctx_set_kernel variant 1: WG_F_AFTER_SEAL as seal + open launches
   // plan workspace: k_tile block scan, k_transport longest-first order
   DevBuf plan_nb, plan_prefix, plan_tiles, plan_ntiles, plan_tmp, lpt_hist, lpt_order;
   DevBuf lpt_hist2, lpt_order2;  // the open half of a wg_duplex_batch
+  DevBuf lpt_nlong;              // k_lpt_scatter -> k_*_mixed: long packets at the front of lpt_order
 
   int kern = KERN_TRANSPORT;
   // host-API staging
@@ -294,7 +298,7 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
                    uint64_t out_size, uint32_t* status, uint32_t max_len, uint32_t flags, hipStream_t s,
                    uint64_t cap_waves, uint32_t G, DevBuf& lpt_hist, DevBuf& lpt_order, wgt::TransportParams* Pout,
                    uint32_t* grid_out, bool* ordered_out, const wgt::RxTables* rx = nullptr,
-                   bool private_ws = false, bool reuse_order = false) {
+                   bool private_ws = false, bool reuse_order = false, bool allow_mixed = false) {
   bool ordered = false;
   wgt::TransportParams P{};
   P.desc = desc;
@@ -311,6 +315,10 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
 #ifdef WG_DIAG
   P.stamps = g_stamps;
 #endif
+  // mixed lengths with a split (WG_MIXED_SPLIT): one packet per slot, the long ones in 16-lane
+  // slots (k_transport_mixed / k_step_mixed); the grid is an upper bound, the kernel sizes both
+  // parts from the device count of long packets
+  const bool mixed = allow_mixed && !(flags & WG_F_UNIFORM) && c->mixed_split > 0;
   const uint32_t spw = 64u / G;  // slots per wave
   const uint64_t cap_slots = spw * cap_waves;
   uint64_t per_slot = (n + cap_slots - 1) / cap_slots;
@@ -318,6 +326,7 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   // one-packet-per-slot grid would fill more than half the machine, pair packets longest-first
   // (two or more per slot, k_lpt_*): fewer resident waves, but every slot gets a similar share
   if (!(flags & WG_F_UNIFORM) && per_slot < 2 && 2ull * n > cap_slots) per_slot = 2;
+  if (!(flags & WG_F_UNIFORM) && c->mixed_per_slot) per_slot = c->mixed_per_slot;  // WG_MIXED_PER_SLOT (A/B)
 #ifndef WG_PERSISTENT_UNIFORM
   // uniform lengths: one packet per slot and as many waves as that takes; the hardware
   // dispatcher starts each new wave as an old one retires, so a wave's packet-start
@@ -326,8 +335,9 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   // per slot with longest-first order measured 13% slower on C2)
   if (flags & WG_F_UNIFORM) per_slot = 1;
 #endif
+  if (mixed) per_slot = 1;
   const uint32_t waves = (uint32_t)((n + spw * per_slot - 1) / (spw * per_slot));
-  const uint32_t grid = (waves + wgt::TW - 1) / wgt::TW;
+  const uint32_t grid = mixed ? (n + 4u * wgt::TW - 1u) / (4u * wgt::TW) + 2u : (waves + wgt::TW - 1) / wgt::TW;
   P.slots = grid * wgt::TW * spw;
   // mixed lengths: the rounds a slot runs, spread over the 4 issue-priority levels (k_transport),
   // so the waves that have done the least work issue first (C2 +2%); uniform batches keep the
@@ -338,7 +348,8 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   P.prio_step = (flags & WG_F_UNIFORM) ? 0u : pstep;
   if (c->prio_mode == 0) P.prio_step = 0;  // WG_PRIO=0 / 1: issue priority off / on for every batch (A/B)
   else if (c->prio_mode == 1) P.prio_step = pstep;
-  if (!(flags & WG_F_UNIFORM) && per_slot > 1) {  // longest-first order (LPT) for the snake
+  if (mixed && c->prio_mode != 1) P.prio_step = 0;
+  if (!(flags & WG_F_UNIFORM) && (per_slot > 1 || c->mixed_per_slot || mixed)) {  // longest-first order (LPT)
     // reuse_order: the order already in lpt_order (the seal of the same packets, WG_F_AFTER_SEAL);
     // private_ws: buffers owned by the caller's stream (no shared-workspace ordering)
     if (!reuse_order) {
@@ -346,14 +357,17 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
       const uint32_t lgrid = std::max<uint32_t>(1u, std::min<uint32_t>(wgt::LPT_MAX_BLOCKS, (n + 1023u) / 1024u));
       if ((rc = lpt_hist.ensure(sizeof(uint32_t) * wgt::LPT_MAX_BLOCKS * wgt::LPT_BINS)) != WG_OK) return rc;
       if ((rc = lpt_order.ensure(sizeof(uint32_t) * (size_t)n)) != WG_OK) return rc;
+      if (mixed && (rc = c->lpt_nlong.ensure(sizeof(uint32_t))) != WG_OK) return rc;
       if (!private_ws && (rc = ws_acquire(c, s)) != WG_OK) return rc;
       uint32_t* bh = (uint32_t*)lpt_hist.p;
       hipLaunchKernelGGL((wgt::k_lpt_hist<MODE>), dim3(lgrid), dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len, bh);
       hipLaunchKernelGGL((wgt::k_lpt_scatter<MODE>), dim3(lgrid), dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len,
-                         (const uint32_t*)bh, (uint32_t*)lpt_order.p);
+                         (const uint32_t*)bh, (uint32_t*)lpt_order.p, c->mixed_split,
+                         mixed ? (uint32_t*)c->lpt_nlong.p : nullptr);
       HIPTRY(hipGetLastError());
     }
     P.order = (const uint32_t*)lpt_order.p;
+    if (mixed) P.n_long = (const uint32_t*)c->lpt_nlong.p;
     ordered = !private_ws;
   }
   *Pout = P;
@@ -413,11 +427,12 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
   const bool own = own_hist && own_order;  // the caller holds the plan workspace (launch_after_seal)
   int rc = plan_transport<MODE>(c, desc, n, in, in_size, out, out_size, status, max_len, flags, s, cap_waves, G,
                                 own ? *own_hist : c->lpt_hist, own ? *own_order : c->lpt_order, &P, &grid, &ordered,
-                                rx, own, reuse_order);
+                                rx, own, reuse_order, true);
   if (rc != WG_OK) return rc;
   hipEvent_t ev;
   record_start(c, s, &ev);
-  if (G == 16) hipLaunchKernelGGL((wgt::k_transport<MODE, 16>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
+  if (P.n_long) hipLaunchKernelGGL((wgt::k_transport_mixed<MODE>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
+  else if (G == 16) hipLaunchKernelGGL((wgt::k_transport<MODE, 16>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
   else hipLaunchKernelGGL((wgt::k_transport<MODE, 8>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
   const hipError_t e = hipGetLastError();
   record_end(c, s, ev);
@@ -460,11 +475,11 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
     bool os = false, oo = false;
     rc = plan_transport<WG_MODE_SEAL>(c, sb->desc, sb->n, sb->in, sb->in_size, sb->out, sb->out_size, nullptr,
                                       sb->max_len, sb->flags, s, cap, G, c->lpt_hist, c->lpt_order, &PS, &gs, &os,
-                                      nullptr, true, false);
+                                      nullptr, true, false, true);
     if (rc == WG_OK)
       rc = plan_transport<WG_MODE_OPEN>(c, ob->desc, ob->n, ob->in, ob->in_size, ob->out, ob->out_size, ob->status,
                                         ob->max_len, ob->flags & ~WG_F_AFTER_SEAL, s, cap, G, c->lpt_hist,
-                                        c->lpt_order, &PO, &go, &oo, nullptr, true, true);
+                                        c->lpt_order, &PO, &go, &oo, nullptr, true, true, true);
     // one issue-priority schedule over the seal and open halves (the rounds of both)
     if (PS.prio_step) PS.prio_step = PO.prio_step = 2u * PS.prio_step;
     if (rc == WG_OK && (gs != go || PS.slots != PO.slots || PS.order != PO.order))
@@ -475,7 +490,8 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
     if (rc == WG_OK) {
       hipEvent_t ev;
       record_start(c, s, &ev);
-      if (G == 16) hipLaunchKernelGGL(wgt::k_step<16>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+      if (PS.n_long) hipLaunchKernelGGL(wgt::k_step_mixed, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+      else if (G == 16) hipLaunchKernelGGL(wgt::k_step<16>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else hipLaunchKernelGGL(wgt::k_step<8>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       const hipError_t e = hipGetLastError();
       record_end(c, s, ev);
@@ -572,6 +588,8 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
       c->resident_waves[w][k] = (uint32_t)std::max(bl[w][k], 1) * wgt::TW * (uint32_t)prop.multiProcessorCount;
   if (const char* e = getenv("WG_SLOT16")) c->slot16 = atoi(e);
   if (const char* e = getenv("WG_PRIO")) c->prio_mode = atoi(e);
+  if (const char* e = getenv("WG_MIXED_SPLIT")) c->mixed_split = (uint32_t)std::max(0, atoi(e));
+  if (const char* e = getenv("WG_MIXED_PER_SLOT")) c->mixed_per_slot = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_PRIO_LEVELS")) c->prio_levels = (uint32_t)std::min(4, std::max(1, atoi(e)));
   *out = c;
   return WG_OK;
@@ -594,7 +612,7 @@ int wg_ctx_destroy(wg_ctx* c) {
     (void)hipEventDestroy(e.second);
   }
   for (DevBuf* b : {&c->plan_nb, &c->plan_prefix, &c->plan_tiles, &c->plan_ntiles, &c->plan_tmp, &c->lpt_hist,
-                    &c->lpt_order, &c->lpt_hist2, &c->lpt_order2, &c->h_desc, &c->h_in, &c->h_out, &c->h_aad, &c->h_status,
+                    &c->lpt_order, &c->lpt_hist2, &c->lpt_order2, &c->lpt_nlong, &c->h_desc, &c->h_in, &c->h_out, &c->h_aad, &c->h_status,
                     &c->h_keys})
     b->release();
   if (c->stream) (void)hipStreamDestroy(c->stream);

@@ -120,6 +120,8 @@ struct TransportParams {
   uint32_t* status;       // open: per-packet WG_PKT_*
   uint32_t prio_step;     // rounds per issue-priority level (0: no priority changes)
   const RxTables* rx;     // open with WG_F_RX_FILTER: receive-side verdict in the status (else NULL)
+  const uint32_t* n_long; // k_*_mixed: device count of the packets at the front of the order that take
+                          // 16-lane slots (written by k_lpt_scatter); NULL otherwise
 #ifdef WG_DIAG
   uint64_t* stamps;       // diagnostic build only: 10 x u64 per wave (cycles per phase, start/end times)
 #endif
@@ -688,6 +690,64 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
   transport_body<MODE, G>(P, blockIdx.x, wv, img_[wv], rec_[wv], iter);
 }
 
+// ---- mixed-length batches: 16-lane slots for the long packets, 8-lane slots for the rest ----
+// The batch is ordered longest-first (k_lpt_*); the n_long packets at its front (more than
+// `split` rounds of 8 blocks) take 16-lane slots, so no slot runs much more than `split` rounds.
+// Every slot holds ONE packet and the grid has as many workgroups as that takes (more than are
+// resident): the hardware dispatcher starts each new workgroup as an old one retires, longest
+// packets first. Workgroups [0, b16) run the 16-lane body, [b16, b16 + b8) the 8-lane body; the
+// rest of the (host-sized, upper-bound) grid exits at once.
+__device__ __forceinline__ int mixed_part(const TransportParams& P, uint32_t blk, TransportParams& Q, uint32_t& qblk) {
+  const uint32_t nl = min(__builtin_amdgcn_readfirstlane(*(const WG_CONST uint32_t*)P.n_long), P.n);
+  const uint32_t b16 = (nl + 4u * TW - 1u) / (4u * TW);
+  Q = P;
+  if (blk < b16) {
+    Q.n = nl;
+    Q.slots = b16 * TW * 4u;
+    qblk = blk;
+    return 16;
+  }
+  const uint32_t ns = P.n - nl, b8 = (ns + 8u * TW - 1u) / (8u * TW);
+  if (blk - b16 >= b8) return 0;
+  Q.order = P.order + nl;
+  Q.n = ns;
+  Q.slots = b8 * TW * 8u;
+  qblk = blk - b16;
+  return 8;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8))) k_transport_mixed(TransportParams P) {
+  __shared__ uint4 img_[TW][4 * 64];
+  __shared__ SlotRec rec_[TW][8];
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  TransportParams Q;
+  uint32_t qb = 0, iter = 0;
+  const int g = mixed_part(P, blockIdx.x, Q, qb);
+  if (g == 16) transport_body<MODE, 16>(Q, qb, wv, img_[wv], rec_[wv], iter);
+  else if (g == 8) transport_body<MODE, 8>(Q, qb, wv, img_[wv], rec_[wv], iter);
+}
+
+__global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)))
+k_step_mixed(TransportParams S, TransportParams O) {
+  __shared__ uint4 img_[TW][4 * 64];
+  __shared__ SlotRec rec_[TW][8];
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  TransportParams QS, QO;
+  uint32_t qb = 0, qb2 = 0, iter = 0;
+  const int g = mixed_part(S, blockIdx.x, QS, qb);
+  (void)mixed_part(O, blockIdx.x, QO, qb2);  // the same split: the open batch has the seal's lengths
+  if (g == 16) {
+    transport_body<WG_MODE_SEAL, 16>(QS, qb, wv, img_[wv], rec_[wv], iter);
+    asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
+    transport_body<WG_MODE_OPEN, 16>(QO, qb, wv, img_[wv], rec_[wv], iter);
+  } else if (g == 8) {
+    transport_body<WG_MODE_SEAL, 8>(QS, qb, wv, img_[wv], rec_[wv], iter);
+    asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
+    transport_body<WG_MODE_OPEN, 8>(QO, qb, wv, img_[wv], rec_[wv], iter);
+  }
+}
+
 // One launch, two directions (wg_duplex_batch): a node's outgoing batch sealed and its
 // incoming batch opened side by side. Workgroups [0, 2m) alternate seal / open (m = the
 // smaller grid), the rest belong to the larger direction; each half runs exactly the
@@ -772,7 +832,8 @@ __global__ void __launch_bounds__(LPT_THREADS) k_lpt_hist(const wg_pkt* d, uint3
 // order[pos] = packet, keys descending
 template <int MODE>
 __global__ void __launch_bounds__(LPT_THREADS) k_lpt_scatter(const wg_pkt* d, uint32_t n, uint32_t max_len,
-                                                             const uint32_t* bh, uint32_t* order) {
+                                                             const uint32_t* bh, uint32_t* order, uint32_t split,
+                                                             uint32_t* n_long) {
   __shared__ uint32_t all[LPT_MAX_BLOCKS * LPT_BINS];  // every block's histogram (coalesced load)
   __shared__ uint32_t tot[LPT_BINS], base[LPT_BINS];
   for (uint32_t e = threadIdx.x; e < gridDim.x * LPT_BINS; e += LPT_THREADS) all[e] = bh[e];
@@ -811,6 +872,16 @@ __global__ void __launch_bounds__(LPT_THREADS) k_lpt_scatter(const wg_pkt* d, ui
       const uint32_t p = 3u * l + q;
       if (p < LPT_BINS) tot[LPT_BINS - 1u - p] = acc;
       acc += v[q];
+    }
+    // the packets with more than `split` rounds (keys > split) come first: their count is the
+    // exclusive prefix at key `split`
+    if (n_long && blockIdx.x == 0 && split + 1u < LPT_BINS) {
+      const uint32_t p = LPT_BINS - 1u - split;  // position of key `split` in the descending scan
+      if (l == p / 3u) {
+        uint32_t a = inc - own;
+        for (uint32_t q = 0; q < p % 3u; ++q) a += v[q];
+        *n_long = a;
+      }
     }
   }
   __syncthreads();
