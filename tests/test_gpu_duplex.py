@@ -184,12 +184,17 @@ def test_after_seal_ragged_sizes(n, L):
 
 
 @pytest.mark.parametrize("n", [3000, 40000])
-@pytest.mark.parametrize("slot16", ["0", "1"])
-def test_after_seal_mixed_lengths(n, slot16, monkeypatch):
-    """Mixed lengths: 40000 packets take two per slot, so the batch is ordered longest-first once
-    and the open reuses the seal's order. slot16 "1": 16-lane slots (WG_SLOT16, read when the
+@pytest.mark.parametrize("plan", [None, "WG_SLOT16=0", "WG_SLOT16=1", "WG_MIXED_SPLIT=4"])
+def test_after_seal_mixed_lengths(n, plan, monkeypatch):
+    """Mixed lengths, ordered longest-first once for both halves. plan None: the size-based plan
+    (3000 packets: one per slot, 16-lane slots above one round; 40000: 16-lane longest-first
+    pairs); the others force 8-lane pairs, 16-lane pairs or a split at 4 rounds (read when the
     context is created)."""
-    monkeypatch.setenv("WG_SLOT16", slot16)
+    for var in ("WG_SLOT16", "WG_MIXED_SPLIT"):
+        monkeypatch.delenv(var, raising=False)
+    if plan:
+        k, v = plan.split("=")
+        monkeypatch.setenv(k, v)
     W = wg()
     eng = W.Engine(0, key_slots=16)
     try:

@@ -96,10 +96,11 @@ struct wg_ctx {
   // waves resident at once (occupancy) of k_transport<SEAL>, <OPEN> and k_step, with 8-lane [0] and
   // 16-lane [1] slots
   uint32_t resident_waves[2][3] = {{0, 0, 0}, {0, 0, 0}};
-  int slot16 = 0;                         // 16-lane slots for mixed-length batches (WG_SLOT16=1, A/B)
+  int slot16 = -1;                        // mixed batches: -1 planned (slot_plan), 0 / 1 force 8- / 16-lane slots (WG_SLOT16)
   int prio_mode = -1;                     // progress-based issue priority: -1 mixed batches only, 0 off, 1 on (WG_PRIO)
   uint32_t prio_levels = 4;               // priority levels the schedule steps through (WG_PRIO_LEVELS, 1..4)
   uint32_t mixed_per_slot = 0;            // packets per slot for mixed batches (0: planned; WG_MIXED_PER_SLOT, A/B)
+  uint32_t uniform_per_slot = 0;          // packets per slot for uniform batches (0: one; WG_UNIFORM_PER_SLOT, A/B)
   uint32_t mixed_split = 0;               // > 0: mixed batches one packet per slot, packets of more than this
                                           // many 8-block rounds in 16-lane slots (WG_MIXED_SPLIT)
   bool step_two_launches = false;         // wg_ctx_set_kernel variant 1: WG_F_AFTER_SEAL as seal + open launches
@@ -298,7 +299,7 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
                    uint64_t out_size, uint32_t* status, uint32_t max_len, uint32_t flags, hipStream_t s,
                    uint64_t cap_waves, uint32_t G, DevBuf& lpt_hist, DevBuf& lpt_order, wgt::TransportParams* Pout,
                    uint32_t* grid_out, bool* ordered_out, const wgt::RxTables* rx = nullptr,
-                   bool private_ws = false, bool reuse_order = false, bool allow_mixed = false) {
+                   bool private_ws = false, bool reuse_order = false, uint32_t split = 0) {
   bool ordered = false;
   wgt::TransportParams P{};
   P.desc = desc;
@@ -318,14 +319,16 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   // mixed lengths with a split (WG_MIXED_SPLIT): one packet per slot, the long ones in 16-lane
   // slots (k_transport_mixed / k_step_mixed); the grid is an upper bound, the kernel sizes both
   // parts from the device count of long packets
-  const bool mixed = allow_mixed && !(flags & WG_F_UNIFORM) && c->mixed_split > 0;
+  const bool mixed = !(flags & WG_F_UNIFORM) && split > 0;
   const uint32_t spw = 64u / G;  // slots per wave
   const uint64_t cap_slots = spw * cap_waves;
   uint64_t per_slot = (n + cap_slots - 1) / cap_slots;
   // mixed lengths: a slot holding one packet runs as long as the longest packet, so once a
   // one-packet-per-slot grid would fill more than half the machine, pair packets longest-first
-  // (two or more per slot, k_lpt_*): fewer resident waves, but every slot gets a similar share
-  if (!(flags & WG_F_UNIFORM) && per_slot < 2 && 2ull * n > cap_slots) per_slot = 2;
+  // (an even number per slot, k_lpt_*, so the snake deals each slot long and short packets in
+  // turn): about 4 waves per SIMD, every slot with a similar share. Measured on 131072 C2-shaped
+  // packets: 4 per slot (4096 waves) 1,322 GiB/s, 2 per slot (8192 waves) 1,208, 3 per slot 1,148.
+  if (!(flags & WG_F_UNIFORM) && 2ull * n > cap_slots) per_slot = 2 * ((n + cap_slots - 1) / cap_slots);
   if (!(flags & WG_F_UNIFORM) && c->mixed_per_slot) per_slot = c->mixed_per_slot;  // WG_MIXED_PER_SLOT (A/B)
 #ifndef WG_PERSISTENT_UNIFORM
   // uniform lengths: one packet per slot and as many waves as that takes; the hardware
@@ -335,6 +338,7 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   // per slot with longest-first order measured 13% slower on C2)
   if (flags & WG_F_UNIFORM) per_slot = 1;
 #endif
+  if ((flags & WG_F_UNIFORM) && c->uniform_per_slot) per_slot = c->uniform_per_slot;  // WG_UNIFORM_PER_SLOT (A/B)
   if (mixed) per_slot = 1;
   const uint32_t waves = (uint32_t)((n + spw * per_slot - 1) / (spw * per_slot));
   const uint32_t grid = mixed ? (n + 4u * wgt::TW - 1u) / (4u * wgt::TW) + 2u : (waves + wgt::TW - 1) / wgt::TW;
@@ -362,7 +366,7 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
       uint32_t* bh = (uint32_t*)lpt_hist.p;
       hipLaunchKernelGGL((wgt::k_lpt_hist<MODE>), dim3(lgrid), dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len, bh);
       hipLaunchKernelGGL((wgt::k_lpt_scatter<MODE>), dim3(lgrid), dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len,
-                         (const uint32_t*)bh, (uint32_t*)lpt_order.p, c->mixed_split,
+                         (const uint32_t*)bh, (uint32_t*)lpt_order.p, split,
                          mixed ? (uint32_t*)c->lpt_nlong.p : nullptr);
       HIPTRY(hipGetLastError());
     }
@@ -376,9 +380,28 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   return WG_OK;
 }
 
-// Lanes per slot of k_transport / k_step for a batch: 16 for mixed lengths (long packets take half
-// as many rounds, so the longest-first pairs fill 8 waves per SIMD), 8 for uniform batches.
-uint32_t slot_lanes(const wg_ctx* c, uint32_t flags) { return !(flags & WG_F_UNIFORM) && c->slot16 ? 16u : 8u; }
+// How a batch runs (round-3 measurements; S8 = 8-lane slots resident at once,
+// 65536 on MI355X):
+//   uniform lengths: 8-lane slots, one packet each, as many waves as that takes;
+//   mixed, n >= 3/4 S8: 8-lane slots, longest-first pairs (2+ packets per slot, ~4 waves per SIMD);
+//   mixed, n >= 3/8 S8: 16-lane slots, longest-first pairs (the same wave count for half the packets);
+//   mixed, smaller: one packet per slot, every packet of more than one 8-block round in a 16-lane
+//     slot, longest first (k_transport_mixed / k_step_mixed).
+// C2-shaped batches (64..9000 B): 16384 packets 722 -> 1152 GiB/s, 32768 909 -> 1321 against the
+// 8-lane pairs; 65536 stays on them. WG_SLOT16 / WG_MIXED_SPLIT force a plan (A/B).
+struct SlotPlan {
+  uint32_t G;      // lanes per slot
+  uint32_t split;  // > 0: one packet per slot, packets of more than `split` 8-block rounds in 16-lane slots
+};
+SlotPlan slot_plan(const wg_ctx* c, uint32_t flags, uint32_t n) {
+  if (flags & WG_F_UNIFORM) return {8u, 0u};
+  if (c->mixed_split > 0) return {8u, c->mixed_split};
+  if (c->slot16 >= 0) return {c->slot16 ? 16u : 8u, 0u};
+  const uint64_t s8 = 8ull * c->resident_waves[0][0];
+  if (4ull * n >= 3ull * s8) return {8u, 0u};
+  if (8ull * n >= 3ull * s8) return {16u, 0u};
+  return {8u, 1u};
+}
 
 // Transport seal/open through k_transport: persistent slots, 64 / G per wave. Each slot takes
 // ceil(n / resident slots) packets; mixed-length batches are ordered longest-first on
@@ -421,13 +444,14 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
   wgt::TransportParams P{};
   uint32_t grid = 0;
   bool ordered = false;
-  const uint32_t G = slot_lanes(c, flags);
+  const SlotPlan sp = slot_plan(c, flags, n);
+  const uint32_t G = sp.G;
   const uint64_t cap_waves = std::max<uint32_t>(c->resident_waves[G == 16][MODE == WG_MODE_OPEN], wgt::TW);
   if (rx && c->kern != KERN_TRANSPORT) return fail(WG_EINVAL, "WG_F_RX_FILTER needs the transport kernel");
   const bool own = own_hist && own_order;  // the caller holds the plan workspace (launch_after_seal)
   int rc = plan_transport<MODE>(c, desc, n, in, in_size, out, out_size, status, max_len, flags, s, cap_waves, G,
                                 own ? *own_hist : c->lpt_hist, own ? *own_order : c->lpt_order, &P, &grid, &ordered,
-                                rx, own, reuse_order, true);
+                                rx, own, reuse_order, sp.split);
   if (rc != WG_OK) return rc;
   hipEvent_t ev;
   record_start(c, s, &ev);
@@ -468,18 +492,19 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
   int rc;
   if (ordered && (rc = ws_acquire(c, s)) != WG_OK) return rc;
   if (fused) {
-    const uint32_t G = slot_lanes(c, sb->flags);
+    const SlotPlan sp = slot_plan(c, sb->flags, sb->n);
+    const uint32_t G = sp.G;
     const uint64_t cap = std::max<uint32_t>(c->resident_waves[G == 16][2], wgt::TW);
     wgt::TransportParams PS{}, PO{};
     uint32_t gs = 0, go = 0;
     bool os = false, oo = false;
     rc = plan_transport<WG_MODE_SEAL>(c, sb->desc, sb->n, sb->in, sb->in_size, sb->out, sb->out_size, nullptr,
                                       sb->max_len, sb->flags, s, cap, G, c->lpt_hist, c->lpt_order, &PS, &gs, &os,
-                                      nullptr, true, false, true);
+                                      nullptr, true, false, sp.split);
     if (rc == WG_OK)
       rc = plan_transport<WG_MODE_OPEN>(c, ob->desc, ob->n, ob->in, ob->in_size, ob->out, ob->out_size, ob->status,
                                         ob->max_len, ob->flags & ~WG_F_AFTER_SEAL, s, cap, G, c->lpt_hist,
-                                        c->lpt_order, &PO, &go, &oo, nullptr, true, true, true);
+                                        c->lpt_order, &PO, &go, &oo, nullptr, true, true, sp.split);
     // one issue-priority schedule over the seal and open halves (the rounds of both)
     if (PS.prio_step) PS.prio_step = PO.prio_step = 2u * PS.prio_step;
     if (rc == WG_OK && (gs != go || PS.slots != PO.slots || PS.order != PO.order))
@@ -588,6 +613,7 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
       c->resident_waves[w][k] = (uint32_t)std::max(bl[w][k], 1) * wgt::TW * (uint32_t)prop.multiProcessorCount;
   if (const char* e = getenv("WG_SLOT16")) c->slot16 = atoi(e);
   if (const char* e = getenv("WG_PRIO")) c->prio_mode = atoi(e);
+  if (const char* e = getenv("WG_UNIFORM_PER_SLOT")) c->uniform_per_slot = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_MIXED_SPLIT")) c->mixed_split = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_MIXED_PER_SLOT")) c->mixed_per_slot = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_PRIO_LEVELS")) c->prio_levels = (uint32_t)std::min(4, std::max(1, atoi(e)));
