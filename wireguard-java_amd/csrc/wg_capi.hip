@@ -100,6 +100,7 @@ struct wg_ctx {
   int prio_mode = -1;                     // progress-based issue priority: -1 mixed batches only, 0 off, 1 on (WG_PRIO)
   uint32_t prio_levels = 4;               // priority levels the schedule steps through (WG_PRIO_LEVELS, 1..4)
   uint32_t mixed_per_slot = 0;            // packets per slot for mixed batches (0: planned; WG_MIXED_PER_SLOT, A/B)
+  uint32_t uniform16 = 8;                 // uniform batches of n <= S8 / k packets in 16-lane slots (WG_UNIFORM16=k; 0 never)
   uint32_t uniform_per_slot = 0;          // packets per slot for uniform batches (0: one; WG_UNIFORM_PER_SLOT, A/B)
   uint32_t mixed_split = 0;               // > 0: mixed batches one packet per slot, packets of more than this
                                           // many 8-block rounds in 16-lane slots (WG_MIXED_SPLIT)
@@ -382,7 +383,8 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
 
 // How a batch runs (round-3 measurements; S8 = 8-lane slots resident at once,
 // 65536 on MI355X):
-//   uniform lengths: 8-lane slots, one packet each, as many waves as that takes;
+//   uniform lengths: one packet per slot, as many waves as that takes; 8-lane slots, 16-lane ones for
+//     n <= S8 / 8 (8192 x 1420 B: 665 -> 750 GiB/s; 16384: 1085 -> 948, so not above);
 //   mixed, n >= 3/4 S8: 8-lane slots, longest-first pairs (2+ packets per slot, ~4 waves per SIMD);
 //   mixed, n >= 3/8 S8: 16-lane slots, longest-first pairs (the same wave count for half the packets);
 //   mixed, smaller: one packet per slot, every packet of more than one 8-block round in a 16-lane
@@ -394,7 +396,8 @@ struct SlotPlan {
   uint32_t split;  // > 0: one packet per slot, packets of more than `split` 8-block rounds in 16-lane slots
 };
 SlotPlan slot_plan(const wg_ctx* c, uint32_t flags, uint32_t n) {
-  if (flags & WG_F_UNIFORM) return {8u, 0u};
+  if (flags & WG_F_UNIFORM)  // small uniform batches: twice the waves in 16-lane slots (8192 x 1420 B: 665 -> 750 GiB/s)
+    return {c->uniform16 > 0 && (uint64_t)n * c->uniform16 <= 8ull * c->resident_waves[0][0] ? 16u : 8u, 0u};
   if (c->mixed_split > 0) return {8u, c->mixed_split};
   if (c->slot16 >= 0) return {c->slot16 ? 16u : 8u, 0u};
   const uint64_t s8 = 8ull * c->resident_waves[0][0];
@@ -613,6 +616,7 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
       c->resident_waves[w][k] = (uint32_t)std::max(bl[w][k], 1) * wgt::TW * (uint32_t)prop.multiProcessorCount;
   if (const char* e = getenv("WG_SLOT16")) c->slot16 = atoi(e);
   if (const char* e = getenv("WG_PRIO")) c->prio_mode = atoi(e);
+  if (const char* e = getenv("WG_UNIFORM16")) c->uniform16 = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_UNIFORM_PER_SLOT")) c->uniform_per_slot = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_MIXED_SPLIT")) c->mixed_split = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_MIXED_PER_SLOT")) c->mixed_per_slot = (uint32_t)std::max(0, atoi(e));
