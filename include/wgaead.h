@@ -100,7 +100,10 @@ typedef struct wg_ctx wg_ctx;
 int wg_aead_selftest(int device);
 
 /* Create a context bound to HIP device `device` with a key table of
- * `key_slots` 32-byte entries (zero-initialised). */
+ * `key_slots` 32-byte entries (zero-initialised).
+ * Scheduling overrides read here from the environment, for A/B measurements only (none changes
+ * a byte of output): WG_SLOT16=0|1, WG_MIXED_SPLIT=R, WG_UNIFORM16=k, WG_PRIO=0|1 (DESIGN.md §4.1,
+ * §4.3); unset, the transport kernel plans every batch from its size and the WG_F_UNIFORM hint. */
 int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out);
 int wg_ctx_destroy(wg_ctx* ctx); /* zeroes the key table first */
 int wg_ctx_device(const wg_ctx* ctx);

@@ -98,10 +98,7 @@ struct wg_ctx {
   uint32_t resident_waves[2][3] = {{0, 0, 0}, {0, 0, 0}};
   int slot16 = -1;                        // mixed batches: -1 planned (slot_plan), 0 / 1 force 8- / 16-lane slots (WG_SLOT16)
   int prio_mode = -1;                     // progress-based issue priority: -1 mixed batches only, 0 off, 1 on (WG_PRIO)
-  uint32_t prio_levels = 4;               // priority levels the schedule steps through (WG_PRIO_LEVELS, 1..4)
-  uint32_t mixed_per_slot = 0;            // packets per slot for mixed batches (0: planned; WG_MIXED_PER_SLOT, A/B)
   uint32_t uniform16 = 8;                 // uniform batches of n <= S8 / k packets in 16-lane slots (WG_UNIFORM16=k; 0 never)
-  uint32_t uniform_per_slot = 0;          // packets per slot for uniform batches (0: one; WG_UNIFORM_PER_SLOT, A/B)
   uint32_t mixed_split = 0;               // > 0: mixed batches one packet per slot, packets of more than this
                                           // many 8-block rounds in 16-lane slots (WG_MIXED_SPLIT)
   bool step_two_launches = false;         // wg_ctx_set_kernel variant 1: WG_F_AFTER_SEAL as seal + open launches
@@ -330,7 +327,6 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   // turn): about 4 waves per SIMD, every slot with a similar share. Measured on 131072 C2-shaped
   // packets: 4 per slot (4096 waves) 1,322 GiB/s, 2 per slot (8192 waves) 1,208, 3 per slot 1,148.
   if (!(flags & WG_F_UNIFORM) && 2ull * n > cap_slots) per_slot = 2 * ((n + cap_slots - 1) / cap_slots);
-  if (!(flags & WG_F_UNIFORM) && c->mixed_per_slot) per_slot = c->mixed_per_slot;  // WG_MIXED_PER_SLOT (A/B)
 #ifndef WG_PERSISTENT_UNIFORM
   // uniform lengths: one packet per slot and as many waves as that takes; the hardware
   // dispatcher starts each new wave as an old one retires, so a wave's packet-start
@@ -339,7 +335,6 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   // per slot with longest-first order measured 13% slower on C2)
   if (flags & WG_F_UNIFORM) per_slot = 1;
 #endif
-  if ((flags & WG_F_UNIFORM) && c->uniform_per_slot) per_slot = c->uniform_per_slot;  // WG_UNIFORM_PER_SLOT (A/B)
   if (mixed) per_slot = 1;
   const uint32_t waves = (uint32_t)((n + spw * per_slot - 1) / (spw * per_slot));
   const uint32_t grid = mixed ? (n + 4u * wgt::TW - 1u) / (4u * wgt::TW) + 2u : (waves + wgt::TW - 1) / wgt::TW;
@@ -348,13 +343,12 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   // so the waves that have done the least work issue first (C2 +2%); uniform batches keep the
   // default oldest-first arbitration (the same schedule cost C1 2%)
   const uint32_t max_rounds = (host_pkt_blocks<WG_MODE_SEAL>(max_len) + G - 1u) / G;
-  const uint32_t lv = c->prio_levels;
-  const uint32_t pstep = std::max<uint32_t>(1u, (uint32_t)((per_slot * max_rounds + lv - 1u) / lv));
+  const uint32_t pstep = std::max<uint32_t>(1u, (uint32_t)((per_slot * max_rounds + 3u) / 4u));
   P.prio_step = (flags & WG_F_UNIFORM) ? 0u : pstep;
   if (c->prio_mode == 0) P.prio_step = 0;  // WG_PRIO=0 / 1: issue priority off / on for every batch (A/B)
   else if (c->prio_mode == 1) P.prio_step = pstep;
   if (mixed && c->prio_mode != 1) P.prio_step = 0;
-  if (!(flags & WG_F_UNIFORM) && (per_slot > 1 || c->mixed_per_slot || mixed)) {  // longest-first order (LPT)
+  if (!(flags & WG_F_UNIFORM) && (per_slot > 1 || mixed)) {  // longest-first order (LPT)
     // reuse_order: the order already in lpt_order (the seal of the same packets, WG_F_AFTER_SEAL);
     // private_ws: buffers owned by the caller's stream (no shared-workspace ordering)
     if (!reuse_order) {
@@ -614,13 +608,15 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   for (int w = 0; w < 2; ++w)
     for (int k = 0; k < 3; ++k)
       c->resident_waves[w][k] = (uint32_t)std::max(bl[w][k], 1) * wgt::TW * (uint32_t)prop.multiProcessorCount;
+  // Scheduling overrides for A/B measurements (tools/ab_args.sh), read once per context; none
+  // changes a byte of output (the parity suite runs each): WG_SLOT16=0|1 (mixed batches in 8- or
+  // 16-lane slots), WG_MIXED_SPLIT=R (mixed batches one packet per slot, packets of more than R
+  // 8-block rounds in 16-lane slots), WG_UNIFORM16=k (uniform batches of at most S8/k packets in
+  // 16-lane slots, 0 never), WG_PRIO=0|1 (issue-priority schedule off / on for every batch).
   if (const char* e = getenv("WG_SLOT16")) c->slot16 = atoi(e);
-  if (const char* e = getenv("WG_PRIO")) c->prio_mode = atoi(e);
-  if (const char* e = getenv("WG_UNIFORM16")) c->uniform16 = (uint32_t)std::max(0, atoi(e));
-  if (const char* e = getenv("WG_UNIFORM_PER_SLOT")) c->uniform_per_slot = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_MIXED_SPLIT")) c->mixed_split = (uint32_t)std::max(0, atoi(e));
-  if (const char* e = getenv("WG_MIXED_PER_SLOT")) c->mixed_per_slot = (uint32_t)std::max(0, atoi(e));
-  if (const char* e = getenv("WG_PRIO_LEVELS")) c->prio_levels = (uint32_t)std::min(4, std::max(1, atoi(e)));
+  if (const char* e = getenv("WG_UNIFORM16")) c->uniform16 = (uint32_t)std::max(0, atoi(e));
+  if (const char* e = getenv("WG_PRIO")) c->prio_mode = atoi(e);
   *out = c;
   return WG_OK;
 }
