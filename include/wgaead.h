@@ -62,7 +62,10 @@ extern "C" {
  *        (SymmetricKeypair.cipher: dst = ct || tag, SymmetricKeypair.java:63-74)
  *  open: reads  in[in_off .. in_off+len+16)         ciphertext || tag
  *        writes out[out_off .. out_off+len)         plaintext, only if the tag verifies;
- *        on a bad tag the plaintext range is zero-filled and status = WG_PKT_BADTAG
+ *        on a bad tag the plaintext range is zero-filled and status = WG_PKT_BADTAG;
+ *        when the plaintext range overlaps in[in_off .. in_off+len+16) (in place, or moved back),
+ *        the tag is verified before any byte is written and a forged packet's bytes stay as they
+ *        were (ChaCha20Poly1305.java:40-56); an overlap that moves the plaintext forward is undefined
  *        (SymmetricKeypair.decipher: L = src.size - 16, SymmetricKeypair.java:76-83)
  *  counter: the 64-bit transport counter (TransportPacket.java:53-55); nonce built on device.
  *  key_slot: index into the context's device key table (wg_keys_set). */

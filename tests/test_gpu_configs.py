@@ -110,35 +110,54 @@ def test_c3_sharded_roundtrip_and_oracle_subset():
         eng.close()
 
 
-def test_in_place_open_bad_tag_zero_fills(engine):
-    """Batch open with in == out (the incoming buffer holds ct, pt is written over it):
-    a good packet decrypts in place; a forged one comes back WG_PKT_BADTAG with its
-    plaintext range zero-filled. The reference leaves the ciphertext of a forged packet in
-    place (ChaCha20Poly1305.java:51-53 throws before decrypting); the batch API documents the
-    zero-fill instead (include/wgaead.h), and the per-packet wg_open1 keeps
-    dst untouched."""
+@pytest.mark.parametrize("shift", [0, -8, -1])
+@pytest.mark.parametrize("uniform", [True, False])
+def test_in_place_open_keeps_forged_packets(engine, shift, uniform):
+    """Batch open whose plaintext range overlaps the ciphertext || tag range (in place, shift 0,
+    or moved back by a few bytes, which a byte-sequential decrypt also allows; a forward move is
+    undefined, as for the reference's sequential cipher): every such packet is verified before
+    any byte is written
+    (verify-first: the tag pass, then a decrypt pass), as ChaCha20Poly1305.java:40-56 verifies
+    before it decrypts. A good packet decrypts in place; a forged one comes back WG_PKT_BADTAG
+    with its ciphertext || tag untouched. Mixed lengths (uniform False) include 0-byte and
+    multi-round packets."""
     torch, dev = _dev()
     W = wg()
-    n, L, S = 4, 300, 320
-    off = np.arange(n, dtype=np.uint64) * (S + 16)
-    desc = W.pack_desc(off, off, np.arange(n, dtype=np.uint64), L, 0)
+    rng = np.random.default_rng(70 + shift)
+    n = 40
+    lengths = np.full(n, 300, np.int64) if uniform else rng.integers(0, 3000, n).astype(np.int64)
+    lengths[3] = 0 if not uniform else lengths[3]
+    S = ((lengths + 16 + 15) // 16) * 16 + 32
+    off = (np.concatenate([[0], np.cumsum(S)[:-1]]) + 16).astype(np.uint64)
+    total = int(S.sum()) + 64
     keys = splitmix_np(61, 32)
-    pt = splitmix_np(62, n * (S + 16))
-    sealed = np.zeros_like(pt)
-    O.seal_batch(desc, pt, sealed, keys, threads=1)
-    sealed[int(off[2]) + L] ^= 1  # forge packet 2's tag
+    pt = splitmix_np(62 + shift, total)
+    sd = W.pack_desc(off, off, np.arange(n, dtype=np.uint64), lengths, np.zeros(n, np.int64))
+    sealed = pt.copy()
+    O.seal_batch(sd, pt, sealed, keys, threads=1)
+    forged = rng.random(n) < 0.3
+    forged[0], forged[1] = True, False
+    for i in np.nonzero(forged)[0]:
+        sealed[int(off[i]) + int(lengths[i])] ^= 1  # a tag bit
+    od = sd.copy()
+    od["out_off"] = (off.astype(np.int64) + shift).astype(np.uint64)
     engine.set_keys(0, keys.tobytes())
     buf = torch.from_numpy(sealed.copy()).to(dev)
     st = torch.zeros(n, dtype=torch.int32, device=dev)
-    engine.open(torch.from_numpy(W.desc_as_int64(desc)).to(dev), buf, buf, st, L, uniform=True)
+    engine.open(torch.from_numpy(W.desc_as_int64(od)).to(dev), buf, buf, st, int(lengths.max()), uniform=uniform)
     torch.cuda.synchronize()
-    assert st.cpu().tolist() == [0, 0, 1, 0]
+    assert st.cpu().numpy().tolist() == forged.astype(np.int32).tolist()
     got = buf.cpu().numpy()
+    want = sealed.copy()
     for i in range(n):
-        o = int(off[i])
-        want = np.zeros(L, np.uint8) if i == 2 else pt[o:o + L]
-        assert np.array_equal(got[o:o + L], want), i
-        assert np.array_equal(got[o + L:o + L + 16], sealed[o + L:o + L + 16])  # tags untouched
+        o, L = int(off[i]), int(lengths[i])
+        if not forged[i]:
+            want[o + shift:o + shift + L] = pt[o:o + L]
+    for i in range(n):  # packet by packet (a forged packet's bytes, a good one's plaintext)
+        o, L = int(off[i]), int(lengths[i])
+        lo, hi = min(o, o + shift), max(o + L + 16, o + shift + L)
+        assert np.array_equal(got[lo:hi], want[lo:hi]), (i, bool(forged[i]))
+    assert np.array_equal(got, want)
 
 
 def test_batch_argument_contract(engine):

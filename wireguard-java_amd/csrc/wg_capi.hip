@@ -375,6 +375,13 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   return WG_OK;
 }
 
+// An open whose input and output buffers overlap may hold packets whose plaintext overlaps their
+// own ciphertext || tag: it runs the verify-first kernel variant (include/wgaead.h, wg_pkt).
+bool open_overlaps(const uint8_t* in, uint64_t in_size, const uint8_t* out, uint64_t out_size) {
+  const uintptr_t a = (uintptr_t)in, b = (uintptr_t)out;
+  return a < b + out_size && b < a + in_size;
+}
+
 // How a batch runs (round-3 measurements; S8 = 8-lane slots resident at once,
 // 65536 on MI355X):
 //   uniform lengths: one packet per slot, as many waves as that takes; 8-lane slots, 16-lane ones for
@@ -452,6 +459,17 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
   if (rc != WG_OK) return rc;
   hipEvent_t ev;
   record_start(c, s, &ev);
+  if constexpr (MODE == WG_MODE_OPEN) {
+    if (open_overlaps(in, in_size, out, out_size)) {  // in-place opens verify first (k_transport<OPEN, G, true>)
+      if (P.n_long) hipLaunchKernelGGL((wgt::k_transport_mixed<MODE, true>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
+      else if (G == 16) hipLaunchKernelGGL((wgt::k_transport<MODE, 16, true>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
+      else hipLaunchKernelGGL((wgt::k_transport<MODE, 8, true>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
+      const hipError_t e = hipGetLastError();
+      record_end(c, s, ev);
+      if (e != hipSuccess) return fail(WG_EDEVICE, "k_transport launch: %s", hipGetErrorString(e));
+      return ordered ? ws_release(c, s) : WG_OK;
+    }
+  }
   if (P.n_long) hipLaunchKernelGGL((wgt::k_transport_mixed<MODE>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
   else if (G == 16) hipLaunchKernelGGL((wgt::k_transport<MODE, 16>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
   else hipLaunchKernelGGL((wgt::k_transport<MODE, 8>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
@@ -476,6 +494,7 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
   const bool ordered = !(sb->flags & WG_F_UNIFORM) || !(ob->flags & WG_F_UNIFORM);
   // one k_step launch: both halves on one grid and one order, so every slot opens what it sealed
   const bool fused = c->kern == KERN_TRANSPORT && !c->step_two_launches && sb->max_len == ob->max_len &&
+                     !open_overlaps(ob->in, ob->in_size, ob->out, ob->out_size) &&
                      (sb->flags & WG_F_UNIFORM) == (ob->flags & WG_F_UNIFORM) && !(sb->flags & WG_F_FRAME);
   if (fused) {
     if (sb->n == 0) return WG_OK;
@@ -763,7 +782,8 @@ int wg_duplex_batch(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, void* str
     std::lock_guard<std::mutex> lk(c->mu);
     if ((sb->flags & WG_F_FRAME) && !c->receivers)
       return fail(WG_EINVAL, "WG_F_FRAME without a receiver table (wg_ctx_set_receivers)");
-    const bool fused = !after && c->kern == KERN_TRANSPORT && sb->n && ob->n;
+    const bool fused = !after && c->kern == KERN_TRANSPORT && sb->n && ob->n &&
+                       !open_overlaps(ob->in, ob->in_size, ob->out, ob->out_size);
     if (after && c->kern == KERN_TRANSPORT && sb->n) {
       int rc = launch_after_seal(c, sb, ob, s);
       if (rc != WG_OK) return rc;

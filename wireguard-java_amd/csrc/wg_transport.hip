@@ -189,6 +189,10 @@ __device__ __forceinline__ uint32_t xor8_dpp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
 }
 
+// slot-record flags beyond valid / alignment (SlotRec.meta.w): an open whose plaintext range
+// overlaps its ciphertext || tag range verifies first (no stores) and decrypts in a second pass
+constexpr uint32_t kVerifyFirst = 16u, kDecryptPass = 32u;
+
 // ---- validity of one transport descriptor (shared by seal, open and the framing) ----
 template <int MODE>
 __device__ __forceinline__ bool transport_valid(uint64_t in_off, uint64_t out_off, uint32_t len, uint32_t ks,
@@ -305,11 +309,12 @@ __device__ __forceinline__ uint32_t opaque_lane() {
 // 8 waves per SIMD).
 // iter: rounds this wave has run so far in the launch (the issue-priority schedule spans both
 // halves of a k_step launch).
-template <int MODE, int G = 8>
+template <int MODE, int G = 8, bool VF = false>
 __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_t blk, uint32_t wv, uint4* const img,
                                                SlotRec* const rec, uint32_t& iter) {
   static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
   static_assert(G == 8 || G == 16, "slots of 8 or 16 lanes");
+  static_assert(!VF || MODE == WG_MODE_OPEN, "verify-first is an open variant");
   constexpr uint32_t SH = G == 8 ? 3u : 4u;  // log2 G
   constexpr uint32_t JM = G - 1u;
   if (P.prio_step && iter == 0) __builtin_amdgcn_s_setprio(3);  // first instruction: a fresh wave is never starved
@@ -366,7 +371,11 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
       const bool valid =
           transport_valid<MODE>(in_off, out_off, len, ks, P.max_len, P.key_slots, P.in_size, P.out_size);
       const uintptr_t ia = (uintptr_t)(P.in + in_off), oa = (uintptr_t)(P.out + out_off);
-      const uint32_t al = ((ia & 15u) == 0 ? 2u : 0u) | ((oa & 15u) == 0 ? 4u : 0u) | ((oa & 3u) == 0 ? 8u : 0u);
+      uint32_t al = ((ia & 15u) == 0 ? 2u : 0u) | ((oa & 15u) == 0 ? 4u : 0u) | ((oa & 3u) == 0 ? 8u : 0u);
+      // open with the plaintext range overlapping the ciphertext || tag range (in place): verify the
+      // tag first and decrypt in a second pass, so a forged packet's bytes stay as they were
+      // (ChaCha20Poly1305.java:40-56 verifies before it decrypts)
+      if (VF && valid && len && ia < oa + len && oa < ia + len + 16u) al |= kVerifyFirst;
       // The session key. Vector loads come back in order through the CU's L1, so at a launch's
       // start a key load would queue behind the payload DMA of every wave already running on
       // the CU; when every slot of the wave uses one key (one session per wave: C1, C3) it comes
@@ -465,9 +474,10 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
 #endif
     }
 
-    if (__any(have && round == 0)) {  // round 0: lane 0 of the slot holds the one-time key r || s
+    const bool mac_pass = !VF || !(meta.w & kDecryptPass);  // the second pass of a verify-first open only decrypts
+    if (__any(have && round == 0 && mac_pass)) {  // round 0: lane 0 of the slot holds the one-time key r || s
       const uint32_t lane = opaque_lane(), s = lane >> SH;
-      if (have && round == 0 && (lane & JM) == 0) {
+      if (have && round == 0 && mac_pass && (lane & JM) == 0) {
         rec[s].R0 = make_uint4(x[0], x[1], x[2], x[3]);  // raw r, replaced by R = r^8 below
         rec[s].s = make_uint4(x[4], x[5], x[6], x[7]);
       }
@@ -504,7 +514,8 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
 #endif
             }
 #ifndef WG_ABL_NOSTORE
-            store_chunk(dst + 16u * q, cb, o, oal);
+            if (!VF || (meta.w & (kVerifyFirst | kDecryptPass)) != kVerifyFirst)
+              store_chunk(dst + 16u * q, cb, o, oal);
 #endif
           }
         }
@@ -524,8 +535,8 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
 
     // ---- round 0: r^1..r^G (lane j gets r^(j+1)), R = r^G, W = r^(G-j) --------------------
     // (after the XOR phase, so the 32 registers of keystream and payload are free again)
-    if (__any(have && round == 0)) {
-      if (have && round == 0) {
+    if (__any(have && round == 0 && mac_pass)) {
+      if (have && round == 0 && mac_pass) {
         const uint32_t lane = opaque_lane(), s = lane >> SH, j = lane & JM;
         const uint4 rr = rec[s].R0;
         uint32_t y[5];
@@ -564,7 +575,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
 #ifdef WG_ABL_NOPOLY
     if (false) {
 #else
-    if (have && (meta.w & 1u)) {
+    if (have && (meta.w & 1u) && mac_pass) {
 #endif
       const uint32_t lane = opaque_lane(), s = lane >> SH, j = lane & JM;
       {
@@ -606,34 +617,37 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
       if (done) {  // slot-uniform: every lane of a finishing slot is here
         const uint32_t lane = opaque_lane(), s = lane >> SH, j = lane & JM;
         const bool valid = meta.w & 1u;
-        if (valid) {
-          if (j == JM && ((len + 15u) >> 4) >= 4u * G * round + 4u * G - 4u) {  // length block not taken in the loop
-            const uint4 q0 = rec[s].R0, q1 = rec[s].R1, q2 = rec[s].R2;
-            const uint32_t R[5] = {q0.x, q0.y, q0.z, q0.w, q1.x};
-            const uint32_t Rs[5] = {0u, q1.y, q1.z, q1.w, q2.x};
-            poly_mul(acc, R, Rs);
-            acc[2] += (len << 12) & M26;  // le64(len) at bit 64: limb 2 holds bits 52..77
-            acc[3] += len >> 14;
-            acc[4] += 1u << 24;
-          }
+        if (mac_pass) {
+          if (valid) {
+            if (j == JM && ((len + 15u) >> 4) >= 4u * G * round + 4u * G - 4u) {  // length block not taken in the loop
+              const uint4 q0 = rec[s].R0, q1 = rec[s].R1, q2 = rec[s].R2;
+              const uint32_t R[5] = {q0.x, q0.y, q0.z, q0.w, q1.x};
+              const uint32_t Rs[5] = {0u, q1.y, q1.z, q1.w, q2.x};
+              poly_mul(acc, R, Rs);
+              acc[2] += (len << 12) & M26;  // le64(len) at bit 64: limb 2 holds bits 52..77
+              acc[3] += len >> 14;
+              acc[4] += 1u << 24;
+            }
 #ifndef WG_ABL_NOFINISH
-          uint32_t Ws[5];
-          poly_scale5(W, Ws);
-          poly_mul(acc, W, Ws);
+            uint32_t Ws[5];
+            poly_scale5(W, Ws);
+            poly_mul(acc, W, Ws);
 #endif
-        }
+          }
 #pragma unroll
-        for (int i = 0; i < 5; ++i) {  // slot sum (every lane of the slot ends with it)
-          acc[i] += xor1_dpp(acc[i]);
-          acc[i] += xor2_dpp(acc[i]);
-          acc[i] += xor4_dpp(acc[i]);
-          if constexpr (G == 16) acc[i] += xor8_dpp(acc[i]);
+          for (int i = 0; i < 5; ++i) {  // slot sum (every lane of the slot ends with it)
+            acc[i] += xor1_dpp(acc[i]);
+            acc[i] += xor2_dpp(acc[i]);
+            acc[i] += xor4_dpp(acc[i]);
+            if constexpr (G == 16) acc[i] += xor8_dpp(acc[i]);
+          }
         }
         const uint4 ad = rec[s].addr;
         const uint8_t* inp = P.in + ((uint64_t)ad.x | ((uint64_t)ad.y << 32));
         uint8_t* outp = P.out + ((uint64_t)ad.z | ((uint64_t)ad.w << 32));
         uint32_t bad = valid ? 0u : 1u;
-        if (valid && j == 0) {
+        bool again = false;  // a verify-first open whose tag verified: the decrypt pass comes next
+        if (mac_pass && valid && j == 0) {
           const uint4 sv = rec[s].s;
           uint32_t tag[4];
 #ifndef WG_ABL_NOFINISH
@@ -659,19 +673,29 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         }
         if constexpr (MODE == WG_MODE_OPEN) {
           bad = bcastg<G, 0>(bad);
-          if (j == 0 && P.status) {
-            uint32_t st = bad ? WG_PKT_BADTAG : WG_PKT_OK;
-            if (!bad && P.rx) {  // fused receive-side check on the plaintext this slot wrote
-              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's plaintext stores have landed
-              st = rx_verdict(*P.rx, outp, len, P.desc[pkt].key_slot);
-            }
-            P.status[pkt] = st;
-          }
-          if (bad && valid) {  // scrub the unauthenticated plaintext written by this launch
-            for (uint32_t i = j; i < len; i += G) outp[i] = 0;
-          }
+          again = VF && mac_pass && !bad && (meta.w & kVerifyFirst);
         }
-        have = false;
+        if constexpr (MODE == WG_MODE_OPEN) {
+          if (again) {  // decrypt pass: the same rounds again, keystream XOR and stores only
+            if (j == 0) rec[s].meta.w = meta.w | kDecryptPass;
+            round = ~0u;  // incremented to 0 below
+          } else {
+            if (j == 0 && P.status) {
+              uint32_t st = bad ? WG_PKT_BADTAG : WG_PKT_OK;
+              if (!bad && P.rx) {  // fused receive-side check on the plaintext this slot wrote
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's plaintext stores have landed
+                st = rx_verdict(*P.rx, outp, len, P.desc[pkt].key_slot);
+              }
+              P.status[pkt] = st;
+            }
+            if (bad && valid && (!VF || !(meta.w & kVerifyFirst))) {  // scrub the unauthenticated plaintext written
+              for (uint32_t i = j; i < len; i += G) outp[i] = 0;
+            }
+            have = false;
+          }
+        } else {
+          have = false;
+        }
       }
     }
     if (have) ++round;
@@ -681,13 +705,15 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
   WG_PH_STORE(blk * TW + wv);
 }
 
-template <int MODE, int G = 8>
+// VF: an open whose input and output buffers overlap (the host checks the two ranges): packets
+// that overlap themselves verify first (kVerifyFirst); every other launch takes the one-pass body
+template <int MODE, int G = 8, bool VF = false>
 __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8))) k_transport(TransportParams P) {
   __shared__ uint4 img_[TW][4 * 64];  // 4 KB per wave: [chunk q][lane] = the round's payload / MAC input
   __shared__ SlotRec rec_[TW][8];     // 1 KB per wave
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t iter = 0;
-  transport_body<MODE, G>(P, blockIdx.x, wv, img_[wv], rec_[wv], iter);
+  transport_body<MODE, G, VF>(P, blockIdx.x, wv, img_[wv], rec_[wv], iter);
 }
 
 // ---- mixed-length batches: 16-lane slots for the long packets, 8-lane slots for the rest ----
@@ -716,7 +742,7 @@ __device__ __forceinline__ int mixed_part(const TransportParams& P, uint32_t blk
   return 8;
 }
 
-template <int MODE>
+template <int MODE, bool VF = false>
 __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8))) k_transport_mixed(TransportParams P) {
   __shared__ uint4 img_[TW][4 * 64];
   __shared__ SlotRec rec_[TW][8];
@@ -724,8 +750,8 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
   TransportParams Q;
   uint32_t qb = 0, iter = 0;
   const int g = mixed_part(P, blockIdx.x, Q, qb);
-  if (g == 16) transport_body<MODE, 16>(Q, qb, wv, img_[wv], rec_[wv], iter);
-  else if (g == 8) transport_body<MODE, 8>(Q, qb, wv, img_[wv], rec_[wv], iter);
+  if (g == 16) transport_body<MODE, 16, VF>(Q, qb, wv, img_[wv], rec_[wv], iter);
+  else if (g == 8) transport_body<MODE, 8, VF>(Q, qb, wv, img_[wv], rec_[wv], iter);
 }
 
 __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)))
