@@ -502,7 +502,8 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
           if (16u * q < nbytes) {
             const uint32_t cb = min(16u, nbytes - 16u * q);  // valid bytes in this chunk
             uint4 v = img[64u * q + lane];  // payload (the compiler waits for the DMA before this read)
-            if (cb < 16u) v = mask_chunk(v, cb);
+            // open: the MAC input is the zero-padded ciphertext; seal masks the ciphertext below instead
+            if (MODE == WG_MODE_OPEN && cb < 16u) v = mask_chunk(v, cb);
             if constexpr (MODE == WG_MODE_OPEN) {
               if (cb < 16u) img[64u * q + lane] = v;  // the MAC input is the zero-padded ciphertext
             }
