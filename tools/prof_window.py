@@ -85,6 +85,11 @@ def trace(args):
     out["frac_from_profile"] = round(alg / (span_us / b["steps"] * 1e-6) / 8.0e12, 4)
     out["frac_vs_bench"] = round(out["frac_from_profile"] / b["roofline"]["frac"], 4)
     out["span_le_bench_ms_per_step"] = span_us / b["steps"] * 1e-3 <= b["ms_per_step"]
+    # the same fraction from the kernels' own durations: under rocprofv3 the host can take longer to
+    # enqueue a step than the GPU takes to run it (the profiler intercepts every dispatch), and
+    # then the span holds idle gaps that the unprofiled bench does not have
+    out["frac_from_kernel_time"] = round(alg / (busy_us / b["steps"] * 1e-6) / 8.0e12, 4)
+    out["host_bound_under_profiler"] = span_us > 1.05 * busy_us
     return out
 
 
