@@ -346,7 +346,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # under torchrun (WORLD_SIZE set) the ranks always form an RCCL group, one rank included, so the
+    # rendezvous, barriers and gathers of the multi-GPU line run on the GPU path at any N
+    use_dist = "WORLD_SIZE" in os.environ
+    if use_dist:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
@@ -437,7 +440,7 @@ def main():
     # HIP events on the stream the kernels are launched on (torch's current stream,
     # which Engine passes to wg_seal_batch / wg_open_batch), around the whole region
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -448,7 +451,7 @@ def main():
     ev1.record()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = t1 - t0
     gpu_step_ms = ev0.elapsed_time(ev1) / args.steps  # = t_seal + t_open (back-to-back launches), or t_duplex
@@ -491,10 +494,10 @@ def main():
     launches = 1 if (args.mode == "duplex" or fused_step) else 2
     # this rank's own figures, gathered before the max-over-ranks reduction (BASELINE configs[3]:
     # per-GPU and aggregate GiB/s)
-    per_gpu = D.gather_per_rank(dist if world > 1 else None, dev, {
+    per_gpu = D.gather_per_rank(dist if use_dist else None, dev, {
         "elapsed_s": elapsed, "payload_bytes": payload * args.steps, "packets": n, "seal_ms": seal_ms,
         "open_ms": open_ms, "kernel_ms": gpu_step_ms / launches})
-    if world > 1:
+    if use_dist:
         (elapsed, seal_ms, open_ms, gpu_step_ms), payload_all, all_ok = D.reduce_report(
             dist, dev, [elapsed, seal_ms, open_ms, gpu_step_ms], payload, ok_status and ok_data)
     else:
@@ -559,7 +562,7 @@ def main():
             line["cpu_baseline"] = cpu_baseline(lengths, slots, counters, keys)
         print(json.dumps(line), flush=True)
     eng.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
     if not all_ok:
         sys.exit(3)
