@@ -1,6 +1,8 @@
 # per-packet server: waves exit on their own idle time (old, wireguard-java_amd/ppold) vs only when
 # no wave has served for idle_us (new; spin1k: callers sleep after 1,024 checks instead of 4,096),
 # alternating on one box; callers 16 / 64 / 128
+# (wireguard-java_amd/ppold/libwgaead.so: the csrc tree with the variant under test swapped back, built by hand with
+# the Makefile's hipcc line; without it both slots load the product library, i.e. a control run)
 set -o pipefail
 mkdir -p gpurun_out/ppidle
 timeout -k 10 300 python -u -m pytest tests/test_batcher.py -x -q -m gpu --timeout 120 --timeout-method thread \
