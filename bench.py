@@ -25,13 +25,15 @@ child processes, before anything touches the GPU), waits for them and exits with
 first failing rank's status. Rank 0 prints the JSON line.
 
 The JSON line also carries:
-  roofline      the transport kernel (k_wave, seal and open launches) against the
-                8 TB/s HBM peak: achieved = sum(4L + 32) per step / GPU time per step
+  roofline      the transport kernel (k_step: one launch that seals and then opens the batch)
+                against the 8 TB/s HBM peak: achieved = sum(4L + 32) per step / GPU time per step
                 (SURVEY.md §8d), GPU time from HIP events on the launch stream around
                 the timed region; `traffic` = HBM bytes per launch from the committed
                 rocprofv3 PMC summary (profiles/pmc_*.json) when present
   cpu_baseline  the CPU restatement (oracle/liboracle.so, bit-exact to the
                 reference) timed on this host's cores, rank 0, N = 1 only
+  oracle_sample ct||tag of 2048 seeded packets of the timed batch against the oracle (rank 0,
+                N = 1, after the timed region); a mismatch makes `verified` false
 Before the W warmup steps every rank runs untimed steps for --ramp-ms (default 150 ms)
 so the GPU clocks have ramped before the timed region (ramp_ms in the JSON line).
 """
@@ -96,6 +98,21 @@ def build_workload(name: str, rank: int, world: int, packets: int = 0, keys: int
         nkeys = len(D.session_shard(sessions, rank, world))
         return lengths, slots, counters, nkeys, f"C3: {total} x {L}B total over {world} GPU(s), sharded by session", True
     raise SystemExit(f"unknown workload {name}")
+
+
+def oracle_sample_check(sample, keys):
+    """The checker, after the timed region: the ciphertext || tag the timed kernel wrote for a seeded
+    sample of packets, compared byte for byte with the CPU restatement sealing the same plaintext
+    (`verified` alone is open(seal(x)) == x, which a self-consistent seal bug would pass)."""
+    from oracle import oracle as O
+    desc, pt, ct = sample
+    ref = np.zeros_like(ct)
+    O.seal_batch(desc, pt, ref, keys, threads=max(1, min(16, os.cpu_count() or 1)))
+    L = desc["len"].astype(np.int64)
+    ok = all(np.array_equal(ct[int(o):int(o) + int(l) + 16], ref[int(o):int(o) + int(l) + 16])
+             for o, l in zip(desc["in_off"], L))
+    return {"packets": int(len(desc)), "bit_exact": bool(ok),
+            "what": "ct||tag of a seeded sample of the timed batch vs oracle/liboracle.so sealing its plaintext"}
 
 
 def cpu_baseline(lengths, slots, counters, keys, budget_s: float = 1.5):
@@ -482,6 +499,32 @@ def main():
         ok_data = bool(torch.equal(back[mask], pt[mask]))
         del idx, pkt, mask
 
+    # a seeded sample of the timed batch, copied out for the oracle check (rank 0, N = 1, next to the
+    # CPU baseline; the oracle is the checker, never the thing measured)
+    sample = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        pick = np.sort(np.random.default_rng(4242).choice(n, min(n, 2048), replace=False))
+        sd = desc[pick].copy()
+        SS = S[pick]
+        so = np.concatenate([[0], np.cumsum(SS)[:-1]]).astype(np.uint64)
+        sd["in_off"] = sd["out_off"] = so
+        spt = np.zeros(int(SS.sum()), np.uint8)
+        sct = np.zeros(int(SS.sum()), np.uint8)
+        if uniform:  # equal strides: gather the sampled rows on the device (C3's buffers are 12 GB)
+            s0 = int(S[0])
+            idx = torch.from_numpy(pick.astype(np.int64)).to(dev)
+            spt[:] = pt.view(n, s0).index_select(0, idx).cpu().numpy().reshape(-1)
+            sct[:] = ct.view(n, s0).index_select(0, idx).cpu().numpy().reshape(-1)
+            del idx
+        else:
+            pt_h, ct_h = pt.cpu().numpy(), ct.cpu().numpy()
+            for k, i in enumerate(pick):
+                o, ln = int(off[i]), int(lengths[i])
+                spt[int(so[k]):int(so[k]) + ln] = pt_h[o:o + ln]
+                sct[int(so[k]):int(so[k]) + ln + 16] = ct_h[o:o + ln + 16]
+            del pt_h, ct_h
+        sample = (sd, spt, sct)
+
     # achievable streaming bandwidth for context: a device-to-device copy of the
     # plaintext buffer, read + write bytes per copy time (after the check above, untimed)
     copy_ms = train(lambda: back.copy_(pt))
@@ -560,6 +603,10 @@ def main():
                                      "frac": round(rate / VALU_PEAK_WIPS, 4), "source": "SQ_INSTS_VALU, profiles/pmc_*.json"}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(lengths, slots, counters, keys)
+            line["oracle_sample"] = oracle_sample_check(sample, keys)
+            if not line["oracle_sample"]["bit_exact"]:
+                all_ok = False
+                line["verified"] = False
         print(json.dumps(line), flush=True)
     eng.close()
     if use_dist:

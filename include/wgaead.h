@@ -50,6 +50,8 @@ extern "C" {
 #define WG_PKT_BADIP 4u     /* IP version nibble not 4 or 6, or too short for the destination address */
 #define WG_PKT_FILTERED 5u  /* destination outside the key slot's AllowedIPs filter */
 #define WG_PKT_REPLAY 6u    /* counter replayed, too old for the window, or >= 2^64 - 2^13 - 1 */
+/* a queued packet (wg_submit_*) whose batch could not run (launch or stream error) */
+#define WG_PKT_FAILED 255u
 
 #define WG_TAG_SIZE 16   /* Crypto.ChaChaPoly1305Overhead (NOISE/crypto/Crypto.java:14) */
 #define WG_NONCE_SIZE 12 /* Crypto.ChaChaPoly1305NonceSize (NOISE/crypto/Crypto.java:13) */
@@ -251,15 +253,20 @@ int wg_parse_open(wg_ctx* ctx, const uint8_t* wire_dev, uint64_t wire_size, cons
  *   returns WG_OK, or 1 for a bad tag (dst untouched, as NOISE/crypto/ChaCha20Poly1305.java:51-55).
  *   Thread-safe and synchronous per call (the per-packet ForkJoinPool fan-out of
  *   TransportManager.java:41,79,152-158), served without a kernel launch per packet: the
- *   packet (with its key, from a host mirror of the key table) goes into a slot of a pinned
- *   ring, and a persistent device kernel (k_pp: one wave per packet in flight) polls the
- *   ring over PCIe, seals/opens the packet and writes the result and a completion word back
- *   into pinned memory, on which the caller spins. The kernel leaves the device after idle_us
- *   without work (and after at most 250 ms) and the next call relaunches it. Packets longer
- *   than 4080 bytes (past the reference pipeline's 4-KB buffers) take the host batch path.
- * wg_batcher_config(ctx, waves, idle_us): waves of that kernel (1..64, default 16; tickets go
- *   round-robin to waves) and its idle timeout (µs, default 20000; 0 = default). Changing the
- *   wave count stops a running server first (no call may be in flight).
+ *   packet (with its key, from a host mirror of the key table) goes into any free entry of a
+ *   pinned 512-entry ring and is published by toggling the entry's doorbell bit; a persistent
+ *   device kernel (k_pp, W waves, wave w owning entries [w 512/W, (w+1) 512/W)) polls the
+ *   doorbells over PCIe, serves every published entry of its range in any order, and writes the
+ *   result and a completion word back into pinned memory, on which the caller spins. A caller
+ *   held up between claiming and publishing delays no other call. The kernel leaves the device
+ *   as a whole after idle_us without work anywhere in it (and after at most 250 ms) and the next
+ *   call relaunches it. A call that fails after publishing (a refused launch) leaves its entry to
+ *   the next server, which completes it; the entry is then reused. Packets longer than 4080 bytes
+ *   (past the reference pipeline's 4-KB buffers) take the host batch path.
+ * wg_pp_config(ctx, waves, idle_us): waves of that kernel (a power of two, 1..64, default 16) and
+ *   its idle timeout (µs, default 20000; 0 = default). Changing it stops a running server first.
+ * wg_batcher_config(ctx, max_batch, window_us): the round-2 batcher's knobs; accepted and ignored
+ *   (the persistent server has no batch size or window).
  * wg_batcher_stats: server launches and packets served by the per-packet path.
  * wg_seal_host / wg_open_host: a batch in host memory (tun ring in, UDP ring out).
  *   If `in` and `out` are pinned, device-mapped host memory (wg_host_alloc /
@@ -323,12 +330,57 @@ int wg_rx_check(wg_ctx* ctx, const wg_pkt* desc_dev, uint32_t n, const uint8_t* 
 
 int wg_seal1(wg_ctx* ctx, uint32_t key_slot, uint64_t counter, const uint8_t* pt, uint32_t len, uint8_t* out);
 int wg_open1(wg_ctx* ctx, uint32_t key_slot, uint64_t counter, const uint8_t* in, uint32_t len, uint8_t* pt);
-int wg_batcher_config(wg_ctx* ctx, uint32_t waves, uint32_t idle_us);
+int wg_pp_config(wg_ctx* ctx, uint32_t waves, uint32_t idle_us);
+int wg_batcher_config(wg_ctx* ctx, uint32_t max_batch, uint32_t window_us);
 int wg_batcher_stats(wg_ctx* ctx, uint64_t* launches, uint64_t* packets);
 int wg_seal_host(wg_ctx* ctx, const wg_pkt* desc_host, uint32_t n, const uint8_t* in_host, uint64_t in_size,
                  uint8_t* out_host, uint64_t out_size, uint32_t max_len, uint32_t flags);
 int wg_open_host(wg_ctx* ctx, const wg_pkt* desc_host, uint32_t n, const uint8_t* in_host, uint64_t in_size,
                  uint8_t* out_host, uint64_t out_size, uint32_t* status_host, uint32_t max_len, uint32_t flags);
+/* ---- asynchronous batch submission -----------------------
+ * The reference's TransportManager hands every packet to a ForkJoinPool worker that calls
+ * cipher / decipher synchronously and then queues the result for the UDP / tun worker
+ * (TransportManager.java:41,70-93,137-158; EstablishedSession.java:88-90). A queue replaces
+ * that synchronous call: producers enqueue packets and return at once, one host thread per
+ * queue batches whatever is waiting into k_transport launches over a pinned, device-mapped
+ * ring (zero-copy), and the consumer reaps the results from a completion queue.
+ *   wg_queue_create(ctx, mode, capacity, max_len, max_batch, &q): a seal (WG_MODE_SEAL) or open
+ *     (WG_MODE_OPEN) queue of `capacity` slots (rounded up to a power of two; 0 = 65536) for
+ *     payloads of at most max_len bytes (0 = 2032, the reference pipeline's incoming limit;
+ *     at most WG_QUEUE_MAX_LEN), batches of at most max_batch packets (0 = 8192).
+ *   wg_submit_seal(q, key_slot, counter, pt, len, user): copies the plaintext into a free slot
+ *     and queues it; the nonce is LE64(counter) || 0^4 (SymmetricKeypair.java:52-61), the key
+ *     the device key table's key_slot. Blocks only while every slot is in use (until the consumer
+ *     calls wg_reap_done). Thread-safe: any number of producers.
+ *   wg_submit_open(q, key_slot, counter, ct_tag, len, user): the same for ct || tag (len + 16 B).
+ *   wg_reap(q, out, max, timeout_us): up to max completions (waits up to timeout_us for the
+ *     first); returns how many, or a negative error. completion.data points into the queue's
+ *     pinned ring: ct || tag (len + 16 B) for a seal, the plaintext (len B, valid when status is
+ *     WG_PKT_OK; WG_PKT_BADTAG: rejected, ChaCha20Poly1305.java:51-55) for an open. Completions
+ *     come back in batch order, not in submission order.
+ *   wg_reap_done(q, c, n): the consumer is done with these completions (their slots are reused).
+ *   wg_queue_destroy: waits for the batches in flight; unreaped completions are dropped. */
+#define WG_QUEUE_MAX_LEN 16384u
+typedef struct wg_queue wg_queue;
+typedef struct wg_completion {
+  uint64_t user;      /* the submitter's tag */
+  uint64_t counter;
+  uint8_t* data;      /* result in the pinned ring (see above) */
+  uint32_t len;       /* payload bytes */
+  uint32_t status;    /* WG_PKT_OK, WG_PKT_BADTAG (open) or WG_PKT_FAILED */
+  uint32_t key_slot;
+  uint32_t slot;      /* ring slot (handed back by wg_reap_done) */
+  uint64_t submit_ns; /* steady-clock time of the submit (latency accounting) */
+} wg_completion;
+int wg_queue_create(wg_ctx* ctx, int mode, uint32_t capacity, uint32_t max_len, uint32_t max_batch, wg_queue** q);
+int wg_queue_destroy(wg_queue* q);
+int wg_submit_seal(wg_queue* q, uint32_t key_slot, uint64_t counter, const uint8_t* pt, uint32_t len, uint64_t user);
+int wg_submit_open(wg_queue* q, uint32_t key_slot, uint64_t counter, const uint8_t* ct_tag, uint32_t len,
+                   uint64_t user);
+int wg_reap(wg_queue* q, wg_completion* out, uint32_t max, uint32_t timeout_us);
+int wg_reap_done(wg_queue* q, const wg_completion* done, uint32_t n);
+int wg_queue_stats(wg_queue* q, uint64_t* batches, uint64_t* packets);
+
 /* Pinned host rings for the host path (the reference's packet buffers come from
  * a native pool, Pool.java:96; pinning them makes wg_seal_host/wg_open_host zero-copy).
  * wg_host_alloc: page-locked, device-mapped, portable across devices.

@@ -23,27 +23,55 @@ def _dev():
     return torch, torch.device("cuda", 0)
 
 
-def test_c2_full_every_packet(engine):
-    torch, dev = _dev()
-    W = wg()
-    n = 65536
+def _c2_batch(W, n=65536):
+    """configs[2] exactly as bench.py --workload c2 builds it: 64..9000 B, key slot i mod 256,
+    counters i div 256 (each session counting its own packets)."""
     lengths = (64 + splitmix_np(0x5EED2026, 4 * n).view("<u4") % (9000 - 64 + 1)).astype(np.int64)
     S = ((lengths + 16 + 15) // 16) * 16
     off = np.concatenate([[0], np.cumsum(S)[:-1]]).astype(np.uint64)
-    total = int(S.sum())
     desc = W.pack_desc(off, off, np.arange(n, dtype=np.uint64) // 256, lengths, np.arange(n) % 256)
+    return lengths, S, off, int(S.sum()), desc
+
+
+@pytest.mark.parametrize("path", ["separate", "after_seal"])
+def test_c2_full_every_packet(engine, path):
+    """Every C2 packet sealed against the oracle, then opened with 1% forged tags.
+    path "separate": wg_seal_batch then wg_open_batch (k_transport launches);
+    "after_seal": wg_duplex_batch(seal, open | WG_F_AFTER_SEAL), the ONE k_step launch the C2
+    bench line times (8-lane longest-first pairs at 65,536 packets, 9000-B packets up to 18
+    rounds, one issue-priority schedule over both halves): its ciphertext is compared with the
+    oracle byte for byte and its plaintext with the input, so a self-consistent seal bug (a
+    wrong tag the same code recomputes on open) cannot pass."""
+    torch, dev = _dev()
+    W = wg()
+    n = 65536
+    lengths, S, off, total, desc = _c2_batch(W, n)
     keys = splitmix_np(0xC0FFEE, 32 * 256)
     pt = splitmix_np(0x5EED2027, total)
     engine.set_keys(0, keys.tobytes())
     d = torch.from_numpy(W.desc_as_int64(desc)).to(dev)
     dpt = torch.from_numpy(pt).to(dev)
     dct = torch.zeros(total, dtype=torch.uint8, device=dev)
-    engine.seal(d, dpt, dct, 9000)
+    if path == "separate":
+        engine.seal(d, dpt, dct, 9000)
+    else:
+        back = torch.zeros(total, dtype=torch.uint8, device=dev)
+        st = torch.full((n,), 7, dtype=torch.int32, device=dev)
+        engine.duplex(d, dpt, dct, 9000, d, dct, back, st, 9000, uniform=False, after_seal=True)
     torch.cuda.synchronize()
     ref = np.zeros(total, np.uint8)
     O.seal_batch(desc, pt, ref, keys, threads=16)
     got = dct.cpu().numpy()
     assert np.array_equal(got, ref)  # every packet's ct || tag (and untouched slack)
+    if path == "after_seal":
+        assert int(st.abs().sum().item()) == 0
+        b = back.cpu().numpy()
+        want = pt.copy()
+        for i in range(n):
+            o, L = int(off[i]), int(lengths[i])
+            want[o + L:o + int(S[i])] = 0  # slack between packets: never written
+        assert np.array_equal(b, want)
+        del back
     # open every packet, 1% tampered
     bad = np.nonzero(splitmix_np(99, n) < 3)[0]
     for i in bad:
@@ -66,9 +94,11 @@ def test_c2_full_every_packet(engine):
     assert np.array_equal(b, want)
 
 
-def test_c3_sharded_roundtrip_and_oracle_subset():
+@pytest.mark.parametrize("path", ["separate", "after_seal"])
+def test_c3_sharded_roundtrip_and_oracle_subset(path):
     """configs[3] on one GPU: 8M x 1420 B, session s -> rank s mod world (world 1 here),
-    each session counting its packets from 0; 1024 keys."""
+    each session counting its packets from 0; 1024 keys. path "after_seal" is the k_step launch
+    the C3 bench line times (one packet per 8-lane slot, 8M packets)."""
     torch, dev = _dev()
     W = wg()
     D = importlib.import_module("wireguard-java_amd.dist")
@@ -87,10 +117,13 @@ def test_c3_sharded_roundtrip_and_oracle_subset():
         g.manual_seed(1234)
         pt = torch.randint(0, 256, (n * stride,), dtype=torch.uint8, device=dev, generator=g)
         ct = torch.zeros_like(pt)
-        eng.seal(d, pt, ct, L, uniform=True)
         back = torch.zeros_like(pt)
         st = torch.full((n,), 7, dtype=torch.int32, device=dev)
-        eng.open(d, ct, back, st, L, uniform=True)
+        if path == "separate":
+            eng.seal(d, pt, ct, L, uniform=True)
+            eng.open(d, ct, back, st, L, uniform=True)
+        else:
+            eng.duplex(d, pt, ct, L, d, ct, back, st, L, uniform=True, after_seal=True)
         torch.cuda.synchronize()
         assert int(st.abs().sum().item()) == 0
         assert torch.equal(back.view(n, stride)[:, :L], pt.view(n, stride)[:, :L])
@@ -106,6 +139,49 @@ def test_c3_sharded_roundtrip_and_oracle_subset():
         ref = ref.reshape(len(pick), stride)
         assert np.array_equal(sub_ct[:, :L + 16], ref[:, :L + 16])
         del pt, ct, back
+    finally:
+        eng.close()
+
+
+def test_k_step_mixed_c2_shape_default_plan():
+    """wg_duplex_batch(... WG_F_AFTER_SEAL) on 65,536 packets of 64..9000 B over 256 keys with
+    the default size-based plan (8-lane longest-first pairs in ONE k_step launch), on a fresh
+    context, a different seed from test_c2_full_every_packet and odd (4-B aligned) offsets, so the
+    pairs' snake order across the seal -> open boundary is exercised with other lengths; every
+    ciphertext byte against the oracle, every plaintext byte against the input, three calls in a
+    row."""
+    torch, dev = _dev()
+    W = wg()
+    n = 65536
+    lengths = (64 + splitmix_np(0xACE1, 4 * n).view("<u4") % (9000 - 64 + 1)).astype(np.int64)
+    S = ((lengths + 16 + 3) // 4) * 4 + 4
+    off = (np.concatenate([[0], np.cumsum(S)[:-1]]) + 4).astype(np.uint64)
+    total = int(S.sum()) + 8
+    desc = W.pack_desc(off, off, np.arange(n, dtype=np.uint64) // 256 + (1 << 40), lengths, np.arange(n) % 256)
+    keys = splitmix_np(0xBEEF, 32 * 256)
+    pt = splitmix_np(0xF00D, total)
+    eng = W.Engine(0, key_slots=256)
+    try:
+        eng.set_keys(0, keys.tobytes())
+        d = torch.from_numpy(W.desc_as_int64(desc)).to(dev)
+        dpt = torch.from_numpy(pt).to(dev)
+        dct = torch.zeros(total, dtype=torch.uint8, device=dev)
+        back = torch.zeros(total, dtype=torch.uint8, device=dev)
+        st = torch.full((n,), 7, dtype=torch.int32, device=dev)
+        for _ in range(3):
+            back.zero_()
+            eng.duplex(d, dpt, dct, 9000, d, dct, back, st, 9000, uniform=False, after_seal=True)
+        torch.cuda.synchronize()
+        ref = np.zeros(total, np.uint8)
+        O.seal_batch(desc, pt, ref, keys, threads=16)
+        assert np.array_equal(dct.cpu().numpy(), ref)
+        assert int(st.abs().sum().item()) == 0
+        b = back.cpu().numpy()
+        want = np.zeros(total, np.uint8)
+        for i in range(n):
+            o, L = int(off[i]), int(lengths[i])
+            want[o:o + L] = pt[o:o + L]
+        assert np.array_equal(b, want)
     finally:
         eng.close()
 

@@ -1,0 +1,115 @@
+"""Asynchronous batch submission (wg_queue): producers submit packets and return
+at once, one dispatcher thread per queue batches them into k_transport launches over a pinned ring,
+and the consumer reaps completions. The batching replacement for TransportManager's per-packet
+ForkJoinPool submission (TransportManager.java:41,70-93,137-158; EstablishedSession.java:88-90).
+
+-m gpu: every sealed packet against the oracle (oracle/liboracle.so), every opened plaintext against
+the input, forged tags refused; the C producers/consumers harness (tools/queue_bench) bit-checks a
+longer run. Without a GPU: the argument contract."""
+import json
+import os
+import subprocess
+import threading
+
+import numpy as np
+import pytest
+
+from wgtest import oracle, splitmix_bytes, splitmix_np, wg
+
+O = oracle()
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+def test_queue_seal_then_open_bit_exact():
+    W = wg()
+    eng = W.Engine(0, key_slots=16)
+    qs = qo = None
+    try:
+        keys = splitmix_np(2101, 32 * 16)
+        eng.set_keys(0, keys.tobytes())
+        qs, qo = eng.queue("seal", capacity=4096), eng.queue("open", capacity=4096)
+        T, N = 4, 3000
+        sent = {}
+        lock = threading.Lock()
+
+        def producer(t):
+            rng = np.random.default_rng(t)
+            for i in range(N):
+                L = int(rng.integers(0, 2033)) if i % 7 else (0 if i % 2 else 2032)
+                user = (t << 32) | i
+                pt = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+                with lock:
+                    sent[user] = (i % 16, (t << 40) | i, pt)
+                qs.submit(i % 16, (t << 40) | i, pt, user)
+
+        th = [threading.Thread(target=producer, args=(t,)) for t in range(T)]
+        for x in th:
+            x.start()
+        sealed = {}
+        while len(sealed) < T * N:
+            for user, ctr, st, data in qs.reap(4096, 200000):
+                assert st == 0
+                sealed[user] = (ctr, data)
+        for x in th:
+            x.join()
+        assert len(sealed) == T * N
+        for user, (slot, ctr, pt) in sent.items():
+            key = keys[32 * slot:32 * slot + 32].tobytes()
+            assert sealed[user][0] == ctr
+            assert sealed[user][1] == O.c_aead_seal(key, O.transport_nonce(ctr), pt), user
+        # the peer's side: open every packet, about 2% with a flipped tag bit
+        forged = set()
+        for k, (user, (slot, ctr, pt)) in enumerate(sorted(sent.items())):
+            ct = bytearray(sealed[user][1])
+            if k % 50 == 7:
+                ct[len(pt) + (k % 16)] ^= 0x04
+                forged.add(user)
+            qo.submit(slot, ctr, bytes(ct), user)
+        got = {}
+        while len(got) < T * N:
+            for user, ctr, st, data in qo.reap(4096, 200000):
+                got[user] = (st, data)
+        for user, (slot, ctr, pt) in sent.items():
+            st, data = got[user]
+            if user in forged:
+                assert st == W._lib.WG_PKT_BADTAG and data is None, user
+            else:
+                assert st == 0 and data == pt, user
+        b, p = qs.stats()
+        assert p == T * N and 1 <= b <= p
+    finally:
+        for q in (qs, qo):
+            if q is not None:
+                q.close()
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_queue_c_harness_transport_manager_shape():
+    """tools/queue_bench: 16 producer threads submit 1420-B packets to a seal queue, a forwarder
+    reaps them and submits each ct || tag to an open queue, a verifier checks every status and byte
+    of the plaintexts (the reference's FJP workers -> UDP worker -> peer -> tun writer)."""
+    exe = os.path.join(ROOT, "tools", "queue_bench")
+    assert os.path.exists(exe), "tools/queue_bench is built by __graft_entry__.build()"
+    for args in (["16", "20000", "1420"], ["4", "20000", "0"]):
+        r = subprocess.run([exe] + args, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
+        j = json.loads(r.stdout.strip().splitlines()[-1])
+        print(j)
+        assert j["bad"] == 0 and j["packets"] == int(args[0]) * int(args[1])
+
+
+def test_queue_argument_contract():
+    W = wg()
+    lib = W.lib()
+    E = W._lib.WG_EINVAL
+    import ctypes
+    q = ctypes.c_void_p()
+    assert lib.wg_queue_create(None, 0, 0, 0, 0, ctypes.byref(q)) == E
+    assert lib.wg_submit_seal(None, 0, 0, None, 0, 0) == E
+    assert lib.wg_submit_open(None, 0, 0, None, 0, 0) == E
+    assert lib.wg_reap(None, None, 0, 0) == E
+    assert lib.wg_reap_done(None, None, 0) == E
+    assert lib.wg_queue_stats(None, None, None) == E
+    assert lib.wg_queue_destroy(None) == 0

@@ -6,7 +6,14 @@
  *
  * Build: gcc -O2 -pthread -Iinclude -o tools/batcher_bench tools/batcher_bench.c \
  *          -Lwireguard-java_amd -l:libwgaead.so -Wl,-rpath,'$ORIGIN/../wireguard-java_amd'
- * Run:   tools/batcher_bench [threads=16] [calls=10000] [len=1420|0 for mixed 64..1500]
+ * Run:   tools/batcher_bench [threads=16] [calls=10000] [len=1420|0 for mixed 64..1500] [key=value ...]
+ *   gap_us=G        each caller sleeps G us between calls (a quiet tunnel: low call rate)
+ *   hold_us=H       one extra caller, started 20 ms into the run, is held H us between claiming its
+ *                   ring entry and publishing it (test hook WG_PP_TEST_HOLD_*: a caller descheduled
+ *                   mid-call); its latency is reported apart ("held_us") from everyone else's
+ *   fail_launches=F the first F server launches are refused (WG_PP_TEST_FAIL_LAUNCHES); the warm-up
+ *                   call must fail, every timed call must then succeed
+ *   waves=W idle_us=I  wg_pp_config before the first call
  * Output: one JSON line. */
 #include <pthread.h>
 #include <stdint.h>
@@ -22,6 +29,10 @@ static int g_calls, g_len;
 static double* g_lat;          /* [threads][calls] microseconds */
 static uint64_t* g_bytes;      /* payload bytes per thread */
 static int* g_fail;
+static int g_gap_us;
+#define HOLD_COUNTER 0x0D0D0D0D0D0Dull
+static double g_held_us = -1.0;
+static int g_held_rc = 0;
 
 static double now_us(void) {
   struct timespec t;
@@ -58,7 +69,23 @@ static void* worker(void* arg) {
     g_lat[(size_t)t * g_calls + i] = now_us() - t0;
     if (rc != 0) ++g_fail[t];
     g_bytes[t] += L;
+    if (g_gap_us) {
+      struct timespec ts = {g_gap_us / 1000000, (long)(g_gap_us % 1000000) * 1000};
+      nanosleep(&ts, NULL);
+    }
   }
+  return NULL;
+}
+
+static void* held(void* arg) {
+  (void)arg;
+  struct timespec ts = {0, 20 * 1000 * 1000};
+  nanosleep(&ts, NULL);
+  uint8_t pt[1420], ct[1436];
+  memset(pt, 0x5a, sizeof pt);
+  double t0 = now_us();
+  g_held_rc = wg_seal1(g_ctx, 1, HOLD_COUNTER, pt, sizeof pt, ct);
+  g_held_us = now_us() - t0;
   return NULL;
 }
 
@@ -71,9 +98,31 @@ int main(int argc, char** argv) {
   const int T = argc > 1 ? atoi(argv[1]) : 16;
   g_calls = argc > 2 ? atoi(argv[2]) : 10000;
   g_len = argc > 3 ? atoi(argv[3]) : 1420;
+  int hold_us = 0, fail_launches = 0, waves = 16, idle_us = 0;
+  for (int a = 4; a < argc; ++a) {
+    const char* v = strchr(argv[a], '=');
+    if (!v) continue;
+    const int x = atoi(v + 1);
+    if (!strncmp(argv[a], "gap_us=", 7)) g_gap_us = x;
+    else if (!strncmp(argv[a], "hold_us=", 8)) hold_us = x;
+    else if (!strncmp(argv[a], "fail_launches=", 14)) fail_launches = x;
+    else if (!strncmp(argv[a], "waves=", 6)) waves = x;
+    else if (!strncmp(argv[a], "idle_us=", 8)) idle_us = x;
+  }
   if (T < 1 || T > 1024 || g_calls < 2 || g_len < 0 || g_len > 1500) {
-    fprintf(stderr, "usage: batcher_bench [threads] [calls] [len 0..1500]\n");
+    fprintf(stderr, "usage: batcher_bench [threads] [calls] [len 0..1500] [gap_us= hold_us= fail_launches= waves= idle_us=]\n");
     return 2;
+  }
+  char buf[64];
+  if (hold_us) {
+    snprintf(buf, sizeof buf, "%llu", (unsigned long long)HOLD_COUNTER);
+    setenv("WG_PP_TEST_HOLD_COUNTER", buf, 1);
+    snprintf(buf, sizeof buf, "%d", hold_us);
+    setenv("WG_PP_TEST_HOLD_US", buf, 1);
+  }
+  if (fail_launches) {
+    snprintf(buf, sizeof buf, "%d", fail_launches);
+    setenv("WG_PP_TEST_FAIL_LAUNCHES", buf, 1);
   }
   if (wg_ctx_create(0, 64, &g_ctx) != WG_OK) {
     fprintf(stderr, "wg_ctx_create: %s\n", wg_last_error());
@@ -91,13 +140,25 @@ int main(int argc, char** argv) {
   g_bytes = calloc(T, sizeof(uint64_t));
   g_fail = calloc(T, sizeof(int));
   pthread_t th[1024];
-  /* warm-up: one call per thread, untimed */
-  { uint8_t a[64], b[80]; memset(a, 1, 64); wg_seal1(g_ctx, 0, 1ull << 60, a, 64, b); }
+  if (wg_pp_config(g_ctx, (uint32_t)waves, (uint32_t)idle_us) != WG_OK) {
+    fprintf(stderr, "wg_pp_config: %s\n", wg_last_error());
+    return 1;
+  }
+  /* warm-up: one call, untimed (with fail_launches it must be refused) */
+  int warm_rc;
+  { uint8_t a[64], b[80]; memset(a, 1, 64); warm_rc = wg_seal1(g_ctx, 0, 1ull << 60, a, 64, b); }
+  if (fail_launches ? warm_rc == 0 : warm_rc != 0) {
+    fprintf(stderr, "warm-up call: rc %d (%s)\n", warm_rc, wg_last_error());
+    return 1;
+  }
   uint64_t l0 = 0, p0 = 0;
   wg_batcher_stats(g_ctx, &l0, &p0);
   double t0 = now_us();
+  pthread_t hth;
+  if (hold_us) pthread_create(&hth, NULL, held, NULL);
   for (int t = 0; t < T; ++t) pthread_create(&th[t], NULL, worker, (void*)(intptr_t)t);
   for (int t = 0; t < T; ++t) pthread_join(th[t], NULL);
+  if (hold_us) pthread_join(hth, NULL);
   double wall = now_us() - t0;
   uint64_t l1 = 0, p1 = 0;
   wg_batcher_stats(g_ctx, &l1, &p1);
@@ -112,11 +173,13 @@ int main(int argc, char** argv) {
   printf("{\"tool\": \"batcher_bench\", \"threads\": %d, \"calls_per_thread\": %d, \"len\": \"%s\", "
          "\"calls\": %zu, \"failures\": %d, \"wall_s\": %.4f, \"calls_per_s\": %.0f, "
          "\"payload_gib_s\": %.4f, \"lat_us\": {\"p50\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"p999\": %.1f, "
-         "\"max\": %.1f}, \"launches\": %llu, \"mean_batch\": %.1f}\n",
+         "\"max\": %.1f}, \"launches\": %llu, \"mean_batch\": %.1f, \"gap_us\": %d, \"waves\": %d, "
+         "\"fail_launches\": %d, \"hold_us\": %d, \"held_us\": %.1f, \"held_rc\": %d}\n",
          T, g_calls, g_len ? argv[3] : "mixed 64..1500", n, fails, wall * 1e-6, n / (wall * 1e-6),
          bytes / (wall * 1e-6) / (double)(1u << 30), g_lat[n / 2], g_lat[n * 9 / 10], g_lat[n * 99 / 100],
          g_lat[n * 999 / 1000], g_lat[n - 1], (unsigned long long)(l1 - l0),
-         (l1 > l0) ? (double)(p1 - p0) / (double)(l1 - l0) : 0.0);
+         (l1 > l0) ? (double)(p1 - p0) / (double)(l1 - l0) : 0.0, g_gap_us, waves, fail_launches, hold_us,
+         g_held_us, g_held_rc);
   wg_ctx_destroy(g_ctx);
-  return fails ? 1 : 0;
+  return (fails || g_held_rc) ? 1 : 0;
 }

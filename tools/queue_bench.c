@@ -1,0 +1,215 @@
+/* Asynchronous batch submission under the reference's caller shape (TransportManager.java:41,70-93,
+ * 137-158; EstablishedSession.java:88-90): P producer threads (the ForkJoinPool workers) submit
+ * 1420-B packets to a seal queue without waiting (wg_submit_seal); a forwarder thread (the UDP
+ * worker, and the peer's receiving side) reaps the sealed packets and submits each ct||tag to an
+ * open queue (wg_submit_open); a verifier thread (the tun writer) reaps the plaintexts, checks every
+ * status and every byte against what the producer sealed, and gives the slots back.
+ *
+ * Build: make -C tools queue_bench
+ * Run:   tools/queue_bench [producers=16] [packets_per_producer=200000] [len=1420|0 mixed 64..1500]
+ *                          [max_batch=8192]
+ * Output: one JSON line: seal+open payload GiB/s over the whole run (both directions' payload bytes,
+ * as bench.py's cpu_baseline counts them), seal-side rate, latency percentiles per queue (submit ->
+ * reap), batches per queue. Exit status 1 on any failed status or byte mismatch. */
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "wgaead.h"
+
+#define KEYS 64
+#define RB 65536
+static wg_ctx* g_ctx;
+static wg_queue *g_qs, *g_qo;
+static int g_P, g_N, g_len;
+static uint8_t** g_rb;           /* per producer: random bytes the payloads are cut from */
+static _Atomic uint64_t g_fwd, g_ver, g_bad;
+static uint64_t g_total;
+static double *g_lat_s, *g_lat_o; /* sampled latencies, us */
+static _Atomic uint64_t g_ns, g_no;
+#define LAT_SAMPLES (1u << 20)
+
+static uint64_t now_ns(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+
+static uint64_t splitmix(uint64_t* s) {
+  uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+static uint32_t pkt_len(uint64_t user) {
+  if (g_len) return (uint32_t)g_len;
+  uint64_t s = user * 0x2545F4914F6CDD1Dull;
+  return 64u + (uint32_t)(splitmix(&s) % 1437u);
+}
+
+/* payload of packet `user` = (producer t, index i): its 8-byte tag, then bytes of t's buffer */
+static void fill(uint8_t* p, uint64_t user, uint32_t L) {
+  const int t = (int)(user >> 40);
+  const uint32_t i = (uint32_t)user;
+  const uint32_t off = (i * 61u) % (RB - 1600u);
+  memcpy(p, g_rb[t] + off, L);
+  if (L >= 8) memcpy(p, &user, 8);
+}
+
+static void* producer(void* arg) {
+  const int t = (int)(intptr_t)arg;
+  uint8_t pt[1600];
+  for (int i = 0; i < g_N; ++i) {
+    const uint64_t user = ((uint64_t)t << 40) | (uint64_t)i;
+    const uint32_t L = pkt_len(user);
+    fill(pt, user, L);
+    /* the counter: SymmetricKeypair's getAndAdd per session; one session per producer here */
+    if (wg_submit_seal(g_qs, (uint32_t)t % KEYS, (uint64_t)i, pt, L, user) != WG_OK) {
+      fprintf(stderr, "submit_seal: %s\n", wg_last_error());
+      exit(1);
+    }
+  }
+  return NULL;
+}
+
+static void* forwarder(void* arg) {
+  (void)arg;
+  wg_completion c[1024];
+  while (atomic_load(&g_fwd) < g_total) {
+    const int n = wg_reap(g_qs, c, 1024, 1000);
+    if (n < 0) {
+      fprintf(stderr, "reap seal: %s\n", wg_last_error());
+      exit(1);
+    }
+    const uint64_t now = now_ns();
+    for (int k = 0; k < n; ++k) {
+      if (c[k].status != WG_PKT_OK) atomic_fetch_add(&g_bad, 1);
+      const uint64_t j = atomic_fetch_add(&g_ns, 1);
+      if (j < LAT_SAMPLES) g_lat_s[j] = (now - c[k].submit_ns) * 1e-3;
+      /* ct || tag as it would arrive at the peer */
+      if (wg_submit_open(g_qo, c[k].key_slot, c[k].counter, c[k].data, c[k].len, c[k].user) != WG_OK) {
+        fprintf(stderr, "submit_open: %s\n", wg_last_error());
+        exit(1);
+      }
+    }
+    wg_reap_done(g_qs, c, (uint32_t)n);
+    atomic_fetch_add(&g_fwd, (uint64_t)n);
+  }
+  return NULL;
+}
+
+static void* verifier(void* arg) {
+  (void)arg;
+  wg_completion c[1024];
+  uint8_t want[1600];
+  while (atomic_load(&g_ver) < g_total) {
+    const int n = wg_reap(g_qo, c, 1024, 1000);
+    if (n < 0) {
+      fprintf(stderr, "reap open: %s\n", wg_last_error());
+      exit(1);
+    }
+    const uint64_t now = now_ns();
+    for (int k = 0; k < n; ++k) {
+      const uint64_t j = atomic_fetch_add(&g_no, 1);
+      if (j < LAT_SAMPLES) g_lat_o[j] = (now - c[k].submit_ns) * 1e-3;
+      fill(want, c[k].user, c[k].len);
+      if (c[k].status != WG_PKT_OK || c[k].len != pkt_len(c[k].user) || memcmp(c[k].data, want, c[k].len) != 0)
+        atomic_fetch_add(&g_bad, 1);
+    }
+    wg_reap_done(g_qo, c, (uint32_t)n);
+    atomic_fetch_add(&g_ver, (uint64_t)n);
+  }
+  return NULL;
+}
+
+static int cmpd(const void* a, const void* b) {
+  double x = *(const double*)a, y = *(const double*)b;
+  return x < y ? -1 : x > y;
+}
+
+static void pct(double* v, uint64_t n, double out[4]) {
+  if (n == 0) {
+    out[0] = out[1] = out[2] = out[3] = 0;
+    return;
+  }
+  qsort(v, n, sizeof(double), cmpd);
+  out[0] = v[n / 2];
+  out[1] = v[n * 99 / 100];
+  out[2] = v[n * 999 / 1000];
+  out[3] = v[n - 1];
+}
+
+int main(int argc, char** argv) {
+  g_P = argc > 1 ? atoi(argv[1]) : 16;
+  g_N = argc > 2 ? atoi(argv[2]) : 200000;
+  g_len = argc > 3 ? atoi(argv[3]) : 1420;
+  const int max_batch = argc > 4 ? atoi(argv[4]) : 8192;
+  if (g_P < 1 || g_P > 256 || g_N < 1 || g_len < 0 || g_len > 1500) {
+    fprintf(stderr, "usage: queue_bench [producers] [packets_per_producer] [len 0..1500] [max_batch]\n");
+    return 2;
+  }
+  if (wg_ctx_create(0, KEYS, &g_ctx) != WG_OK) {
+    fprintf(stderr, "wg_ctx_create: %s\n", wg_last_error());
+    return 1;
+  }
+  uint8_t keys[KEYS * 32];
+  uint64_t ks = 11;
+  for (int i = 0; i < KEYS * 32; ++i) keys[i] = (uint8_t)splitmix(&ks);
+  if (wg_keys_set(g_ctx, 0, KEYS, keys) != WG_OK ||
+      wg_queue_create(g_ctx, WG_MODE_SEAL, 65536, 1500, (uint32_t)max_batch, &g_qs) != WG_OK ||
+      wg_queue_create(g_ctx, WG_MODE_OPEN, 65536, 1500, (uint32_t)max_batch, &g_qo) != WG_OK) {
+    fprintf(stderr, "setup: %s\n", wg_last_error());
+    return 1;
+  }
+  g_rb = calloc((size_t)g_P, sizeof(uint8_t*));
+  for (int t = 0; t < g_P; ++t) {
+    g_rb[t] = malloc(RB);
+    uint64_t s = 1000 + (uint64_t)t;
+    for (int i = 0; i < RB; ++i) g_rb[t][i] = (uint8_t)splitmix(&s);
+  }
+  g_lat_s = calloc(LAT_SAMPLES, sizeof(double));
+  g_lat_o = calloc(LAT_SAMPLES, sizeof(double));
+  g_total = (uint64_t)g_P * (uint64_t)g_N;
+  uint64_t bytes = 0;
+  for (int t = 0; t < g_P; ++t)
+    for (int i = 0; i < g_N; ++i) bytes += pkt_len(((uint64_t)t << 40) | (uint64_t)i);
+
+  pthread_t th[258];
+  const uint64_t t0 = now_ns();
+  pthread_create(&th[g_P], NULL, forwarder, NULL);
+  pthread_create(&th[g_P + 1], NULL, verifier, NULL);
+  for (int t = 0; t < g_P; ++t) pthread_create(&th[t], NULL, producer, (void*)(intptr_t)t);
+  for (int t = 0; t < g_P; ++t) pthread_join(th[t], NULL);
+  const double t_submit = (now_ns() - t0) * 1e-9;
+  pthread_join(th[g_P], NULL);
+  const double t_sealed = (now_ns() - t0) * 1e-9;
+  pthread_join(th[g_P + 1], NULL);
+  const double wall = (now_ns() - t0) * 1e-9;
+  uint64_t bs = 0, ps = 0, bo = 0, po = 0;
+  wg_queue_stats(g_qs, &bs, &ps);
+  wg_queue_stats(g_qo, &bo, &po);
+  const uint64_t ns = g_ns < LAT_SAMPLES ? g_ns : LAT_SAMPLES, no = g_no < LAT_SAMPLES ? g_no : LAT_SAMPLES;
+  double ls[4], lo[4];
+  pct(g_lat_s, ns, ls);
+  pct(g_lat_o, no, lo);
+  const double gib = (double)(1u << 30);
+  printf("{\"tool\": \"queue_bench\", \"producers\": %d, \"packets\": %llu, \"len\": \"%s\", \"max_batch\": %d, "
+         "\"bad\": %llu, \"wall_s\": %.4f, \"seal_open_gib_s\": %.3f, \"seal_gib_s\": %.3f, "
+         "\"submit_gib_s\": %.3f, \"packets_per_s\": %.0f, "
+         "\"seal_lat_us\": {\"p50\": %.1f, \"p99\": %.1f, \"p999\": %.1f, \"max\": %.1f}, "
+         "\"open_lat_us\": {\"p50\": %.1f, \"p99\": %.1f, \"p999\": %.1f, \"max\": %.1f}, "
+         "\"seal_batches\": %llu, \"seal_mean_batch\": %.1f, \"open_batches\": %llu, \"open_mean_batch\": %.1f}\n",
+         g_P, (unsigned long long)g_total, g_len ? argv[3] : "mixed 64..1500", max_batch,
+         (unsigned long long)g_bad, wall, 2.0 * bytes / wall / gib, bytes / t_sealed / gib, bytes / t_submit / gib,
+         g_total / wall, ls[0], ls[1], ls[2], ls[3], lo[0], lo[1], lo[2], lo[3], (unsigned long long)bs,
+         bs ? (double)ps / bs : 0.0, (unsigned long long)bo, bo ? (double)po / bo : 0.0);
+  wg_queue_destroy(g_qs);
+  wg_queue_destroy(g_qo);
+  wg_ctx_destroy(g_ctx);
+  return g_bad ? 1 : 0;
+}

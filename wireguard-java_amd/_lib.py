@@ -27,6 +27,8 @@ WG_PKT_KEEPALIVE = 3
 WG_PKT_BADIP = 4
 WG_PKT_FILTERED = 5
 WG_PKT_REPLAY = 6
+WG_PKT_FAILED = 255
+WG_QUEUE_MAX_LEN = 16384
 WG_RX_FILTER = 1
 WG_RX_REPLAY = 2
 WG_MAX_FILTERS = 65536
@@ -78,7 +80,14 @@ class WgBatch(ctypes.Structure):
                 ("_reserved", ctypes.c_uint32)]
 
 
-assert ctypes.sizeof(WgBatch) == 64
+class WgCompletion(ctypes.Structure):
+    """wg_completion: one reaped packet of a wg_queue."""
+    _fields_ = [("user", ctypes.c_uint64), ("counter", ctypes.c_uint64), ("data", ctypes.c_void_p),
+                ("len", ctypes.c_uint32), ("status", ctypes.c_uint32), ("key_slot", ctypes.c_uint32),
+                ("slot", ctypes.c_uint32), ("submit_ns", ctypes.c_uint64)]
+
+
+assert ctypes.sizeof(WgBatch) == 64 and ctypes.sizeof(WgCompletion) == 48
 assert ctypes.sizeof(WgPkt) == 32 and ctypes.sizeof(WgAeadDesc) == 64 and ctypes.sizeof(WgPrefix) == 18
 
 # (name, restype, argtypes) for every symbol include/wgaead.h declares
@@ -111,8 +120,16 @@ SIGNATURES = [
     ("wg_rx_check", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U32, _VP]),
     ("wg_seal1", _I, [_VP, _U32, _U64, _VP, _U32, _VP]),
     ("wg_open1", _I, [_VP, _U32, _U64, _VP, _U32, _VP]),
+    ("wg_pp_config", _I, [_VP, _U32, _U32]),
     ("wg_batcher_config", _I, [_VP, _U32, _U32]),
     ("wg_batcher_stats", _I, [_VP, ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
+    ("wg_queue_create", _I, [_VP, _I, _U32, _U32, _U32, ctypes.POINTER(_VP)]),
+    ("wg_queue_destroy", _I, [_VP]),
+    ("wg_submit_seal", _I, [_VP, _U32, _U64, _VP, _U32, _U64]),
+    ("wg_submit_open", _I, [_VP, _U32, _U64, _VP, _U32, _U64]),
+    ("wg_reap", _I, [_VP, ctypes.POINTER(WgCompletion), _U32, _U32]),
+    ("wg_reap_done", _I, [_VP, ctypes.POINTER(WgCompletion), _U32]),
+    ("wg_queue_stats", _I, [_VP, ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
     ("wg_seal_host", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _U32, _U32]),
     ("wg_open_host", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _VP, _U32, _U32]),
     ("wg_host_alloc", _I, [_VP, _U64, ctypes.POINTER(_VP)]),

@@ -565,7 +565,7 @@ int wg_diag_stamps(void* dev_buf) {
 #endif
 
 const char* wg_last_error(void) { return g_err.c_str(); }
-const char* wg_version(void) { return "wgaead 0.2.0 gfx950"; }
+const char* wg_version(void) { return "wgaead 0.3.0 gfx950"; }
 
 int wg_ctx_set_kernel(wg_ctx* c, const char* name, uint32_t lanes, uint32_t variant) {
   (void)lanes;
@@ -884,6 +884,7 @@ int wg_aead_batch(wg_ctx* c, int mode, const wg_aead_desc* desc, uint32_t n, con
 
 #include "wg_host.hip"
 #include "wg_pp.hip"
+#include "wg_queue.hip"
 
 extern "C" {
 

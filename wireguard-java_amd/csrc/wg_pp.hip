@@ -3,27 +3,35 @@
 //
 // The reference seals / opens one packet per synchronous call from ForkJoinPool workers
 // (TransportManager.java:41,79,152-158 -> SymmetricKeypair.java:63-83). Those calls stay
-// per-packet and synchronous. Round 2 batched them under a launcher thread (one kernel
-// launch per batch, ~35 us per round trip, 0.2 GiB/s at 16 callers); here a small
-// persistent kernel (k_pp, W one-wave workgroups) serves them through pinned memory with
-// no launch on the per-packet path:
-//   caller: ticket t (atomic), entry i = t mod kRing; copy the packet + header {mode, len,
-//           counter, key} into in-slot i (pinned, fine-grained host memory), then publish
-//           seq = t + 1 in the slot header (release store, after every other byte);
-//   wave t mod W: polls seq of its next ticket (one system-scope load over PCIe), reads the
-//           header and payload (coalesced system-scope loads into LDS), runs the whole
-//           packet with its 64 lanes (lane j = ChaCha20 block j; 64-strided Poly1305
+// per-packet and synchronous. A small persistent kernel (k_pp, W one-wave workgroups) serves
+// them through pinned memory with no launch on the per-packet path:
+//   caller: claims any FREE entry i of the kRing-entry ring (a CAS on a host-side state word;
+//           no ticket order), copies the packet + header {seq, mode, len, counter, key} into
+//           in-slot i (pinned, fine-grained host memory), then toggles bit i of the doorbell
+//           words (one atomic XOR: the publication, after every other byte);
+//   wave w: owns entries [w E, (w + 1) E), E = kRing / W; polls its doorbell word(s) with one
+//           system-scope load per 64 entries, and serves EVERY entry whose doorbell bit differs
+//           from its acknowledged copy, in index order (out-of-order service: a caller that is
+//           descheduled between claiming and publishing delays nobody but itself). Per entry it
+//           reads the header and payload (coalesced system-scope loads into LDS), runs the
+//           whole packet with its 64 lanes (lane j = ChaCha20 block j; 64-strided Poly1305
 //           Horner over the LDS image with r^64, r-power scan across the wave), writes
-//           ct||tag / plaintext into out-slot i (system-scope stores), waits for them,
-//           then stores done[i] = (t + 1) << 8 | status;
+//           ct||tag / plaintext into out-slot i (system-scope stores), waits for them, then
+//           stores done[i] = seq << 8 | status and flips its acknowledged bit;
 //   caller: spins on done[i] in its own memory, copies the result out (open: only when the
-//           tag verified, so dst stays untouched on a bad tag, ChaCha20Poly1305.java:51-55).
+//           tag verified, so dst stays untouched on a bad tag, ChaCha20Poly1305.java:51-55),
+//           and frees the entry. A call that fails after publishing (a refused launch, a stream
+//           error) leaves its entry ORPHAN: the next server serves it like any other, and the
+//           entry is reclaimed once its completion word shows up, so no entry is ever lost.
 // The session key travels in the slot header from a host mirror of the key table (the
 // reference keeps its keys in host memory too, SymmetricKeypair.java:40-50), so the
 // persistent kernel never reads a device key table that wg_keys_set may rewrite under it.
-// Exit conditions every wave reaches: the context's stop flag, no work for idle_us, or a
-// lifetime of life_ms (then the next caller relaunches). Packets longer than a slot
-// (> kPPMaxLen, beyond the reference pipeline's 4-KB buffers) take the host batch path.
+// Exit is collective: the first wave that finds the whole server idle for idle_us (a shared
+// last-activity stamp), or the launch older than life_ms, raises a quit flag; every wave
+// serves what it has already seen and leaves, the last one raises the host-visible exit flag,
+// and the next caller relaunches. The context's stop flag ends every wave at its next poll.
+// Packets longer than a slot (> kPPMaxLen, beyond the reference pipeline's 4-KB buffers) take
+// the host batch path.
 #pragma once
 
 namespace wgpp {
@@ -54,15 +62,20 @@ struct Ctl {          // pinned, host-written
   uint32_t _pad[15];
 };
 
+constexpr uint32_t kBells = kRing / 64;  // doorbell words: bit i % 64 of word i / 64 toggles per publication
+
 struct PPParams {
   const uint8_t* in;      // device alias: kRing in-slots
   uint8_t* out;           // device alias: kRing out-slots
   uint64_t* done;         // device alias: kRing completion words
+  const uint64_t* bell;   // device alias: kBells doorbell words (host-toggled)
   const Ctl* ctl;         // device alias
   uint64_t* exit_flag;    // device alias (pinned): gen, written by the last wave to exit
-  uint64_t* next;         // device memory: next ticket per wave (kept across launches)
+  uint8_t* ack;           // device memory: per entry, the doorbell parity already served (kept across launches)
   uint32_t* exited;       // device memory: waves exited in this launch (zeroed before it)
-  uint32_t waves;
+  uint32_t* quit;         // device memory: raised by the first wave that decides the server leaves (zeroed)
+  uint64_t* last;         // device memory: s_memrealtime of the last service in this launch (zeroed)
+  uint32_t waves;         // W (power of two, 1..64): wave w owns entries [w E, (w + 1) E), E = kRing / W
   uint32_t gen;
   uint64_t idle_ticks;    // s_memrealtime ticks (100 MHz)
   uint64_t life_ticks;
@@ -95,6 +108,7 @@ constexpr uint32_t kFirstDw = 384;
 // serve as the MAC image (seal: the ciphertext in img_out; open: the ciphertext in img_in).
 __device__ void pp_packet(const Hdr& h, uint64_t ticket, const uint8_t* slot, uint8_t* out, uint64_t* done,
                           uint4* img_in, uint4* img_out) {
+  // ticket: the entry's seq (the caller's unique call number + 1), echoed in the completion word
   const uint32_t lane = threadIdx.x & 63u;
   const bool open = h.mode == WG_MODE_OPEN;
   const uint32_t len = h.len;
@@ -229,7 +243,11 @@ __device__ void pp_packet(const Hdr& h, uint64_t ticket, const uint8_t* slot, ui
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every result byte has landed before done
   PP_STAMP(ticket, 6);
   if (lane == 0)
-    __hip_atomic_store(done, ((ticket + 1u) << 8) | status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(done, (ticket << 8) | status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ uint64_t ld_agent64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void __launch_bounds__(64) k_pp(PPParams P) {
@@ -238,53 +256,97 @@ __global__ void __launch_bounds__(64) k_pp(PPParams P) {
   uint4* const img_in = raw + kHdr / 16;
   const uint32_t w = blockIdx.x;
   const uint32_t lane = threadIdx.x;
-  uint64_t t = P.next[w];
+  const uint32_t E = kRing / P.waves;           // entries of this wave: [base, base + E)
+  const uint32_t base = w * E;
+  const uint32_t nwords = (E + 63u) >> 6;       // doorbell words this wave reads (E >= 64)
+  const uint32_t word0 = base >> 6;
+  const uint32_t sub = base & 63u;              // E < 64: the wave's bits inside one word
+  const uint64_t wmask = E >= 64u ? ~0ull : (((1ull << E) - 1ull) << sub);
+  // acknowledged doorbell parity, lane k holding word k of the wave's range (from the per-entry
+  // bytes the previous launch left)
+  uint64_t ack = 0;
+  for (uint32_t k = 0; k < nwords; ++k) {
+    const uint32_t e = 64u * (word0 + k) + lane;
+    const bool mine = e >= base && e < base + E;
+    const uint64_t m = __ballot(mine && P.ack[e] != 0);
+    if (lane == k) ack = m;
+  }
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  uint64_t last = t0;
   uint32_t backoff = 0;
   for (;;) {
-    const uint32_t i = (uint32_t)(t % kRing);
-    const uint8_t* slot = P.in + (size_t)i * kInSlot;
-    // lane 0: this wave's next ticket published? lane 1: stop flag
+    // lanes 0..nwords-1: doorbell words; lane 32: stop flag
     uint64_t v = 0;
-    if (lane == 0) v = ld_sys64((const uint64_t*)slot);
-    else if (lane == 1) v = ld_sys(&P.ctl->stop);
-    const uint64_t seq = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), 0) << 32) |
-                         __builtin_amdgcn_readlane((uint32_t)v, 0);
-    const uint32_t stop = __builtin_amdgcn_readlane((uint32_t)v, 1);
-    if (seq == t + 1u) {
-      PP_STAMP(t, 0);
-      // header + payload prefix, loaded after seq was seen (the host wrote them before seq):
-      // a system-scope acquire (no stale line of an earlier use of this slot survives in the
-      // CU's caches), then 16-B loads per lane (system-scope dword loads go over PCIe one
-      // request per lane: 7.4 us for these 1536 B, tools/pp_stamps)
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (lane < nwords) v = ld_sys64(P.bell + word0 + lane);
+    else if (lane == 32) v = ld_sys(&P.ctl->stop);
+    const uint32_t stop = __builtin_amdgcn_readlane((uint32_t)v, 32);
+    const uint32_t quit = __hip_atomic_load(P.quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t pend = lane < nwords ? (v ^ ack) & wmask : 0ull;
+    if (stop) break;
+    if (__any(pend != 0)) {
+      // serve every entry pending in this snapshot, in index order
+      for (uint32_t k = 0; k < nwords; ++k) {
+        uint64_t pk = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(pend >> 32), k) << 32) |
+                      __builtin_amdgcn_readlane((uint32_t)pend, k);
+        while (pk) {
+          const uint32_t bit = (uint32_t)__builtin_ctzll(pk);
+          pk &= pk - 1ull;
+          const uint32_t i = 64u * (word0 + k) + bit;
+          const uint8_t* slot = P.in + (size_t)i * kInSlot;
+#ifdef WG_PP_STAMPS
+          const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
+#endif
+          // header + payload prefix, loaded after the doorbell was seen (the host wrote them before
+          // it): a system-scope acquire (no stale line of an earlier use of this slot survives in
+          // the CU's caches), then 16-B loads per lane (system-scope dword loads go over PCIe one
+          // request per lane: 7.4 us for these 1536 B, tools/pp_stamps)
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 #pragma unroll
-      for (uint32_t k = 0; k < kFirstDw / 4; k += 64u)
-        if (k + lane < kFirstDw / 4) raw[k + lane] = ((const uint4*)slot)[k + lane];
-      lds_sync();
-      PP_STAMP(t, 1);
-      Hdr h = *(const Hdr*)raw;
-      h.mode = __builtin_amdgcn_readfirstlane(h.mode);
-      h.len = __builtin_amdgcn_readfirstlane(h.len);
-      if (h.len <= kPPMaxLen && (h.mode == WG_MODE_SEAL || h.mode == WG_MODE_OPEN)) {
-        pp_packet(h, t, slot, P.out + (size_t)i * kOutSlot, P.done + i, img_in, img_out);
-      } else if (lane == 0) {  // refused by the host before publishing; never expected here
-        __hip_atomic_store(P.done + i, ((t + 1u) << 8) | 0xffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          for (uint32_t q = 0; q < kFirstDw / 4; q += 64u)
+            if (q + lane < kFirstDw / 4) raw[q + lane] = ((const uint4*)slot)[q + lane];
+          lds_sync();
+          Hdr h = *(const Hdr*)raw;
+          h.mode = __builtin_amdgcn_readfirstlane(h.mode);
+          h.len = __builtin_amdgcn_readfirstlane(h.len);
+          const uint64_t seq = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(h.seq >> 32)) << 32) |
+                               __builtin_amdgcn_readfirstlane((uint32_t)h.seq);
+#ifdef WG_PP_STAMPS
+          if (lane == 0) g_pp_stamps[seq % 4096u][0] = t_seen;
+#endif
+          PP_STAMP(seq, 1);
+          if (h.len <= kPPMaxLen && (h.mode == WG_MODE_SEAL || h.mode == WG_MODE_OPEN)) {
+            pp_packet(h, seq, slot, P.out + (size_t)i * kOutSlot, P.done + i, img_in, img_out);
+          } else if (lane == 0) {  // refused by the host before publishing; never expected here
+            __hip_atomic_store(P.done + i, (seq << 8) | 0xffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+          lds_sync();
+          if (lane == k) ack ^= 1ull << bit;
+        }
       }
-      lds_sync();
-      t += P.waves;
-      last = __builtin_amdgcn_s_memrealtime();
+      if (lane == 0)
+        __hip_atomic_store(P.last, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       backoff = 0;
+      if (quit) break;  // what this wave had seen is served; new work waits for the relaunch
       continue;
     }
+    if (quit) break;
     const uint64_t now = __builtin_amdgcn_s_memrealtime();
-    if (stop || now - last > P.idle_ticks || now - t0 > P.life_ticks) break;
+    const uint64_t l = ld_agent64(P.last);
+    const uint64_t since = now - (l > t0 ? l : t0);
+    if (since > P.idle_ticks || now - t0 > P.life_ticks) {  // the whole server leaves together
+      if (lane == 0) __hip_atomic_store(P.quit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
     if (backoff < 2u) ++backoff;  // at most 2 x 256 cycles between polls: latency over PCIe traffic
     for (uint32_t k = 0; k < backoff; ++k) __builtin_amdgcn_s_sleep(4);  // 4 x 64 cycles per step
   }
+  // this wave's acknowledged parity back to the per-entry bytes, for the next launch
+  for (uint32_t k = 0; k < nwords; ++k) {
+    const uint64_t a = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(ack >> 32), k) << 32) |
+                       __builtin_amdgcn_readlane((uint32_t)ack, k);
+    const uint32_t e = 64u * (word0 + k) + lane;
+    if (e >= base && e < base + E) P.ack[e] = (uint8_t)((a >> lane) & 1ull);
+  }
   if (lane == 0) {
-    P.next[w] = t;
     __threadfence();
     if (atomicAdd(P.exited, 1u) == P.waves - 1u)
       __hip_atomic_store(P.exit_flag, (uint64_t)P.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -295,27 +357,35 @@ __global__ void __launch_bounds__(64) k_pp(PPParams P) {
 
 namespace {
 
+// host-side state of a ring entry
+enum : uint32_t { kFree = 0, kBusy = 1, kOrphan = 2 };
+
 struct PPServer {
   wg_ctx* c = nullptr;
   hipStream_t stream = nullptr;
-  uint8_t* host = nullptr;   // pinned, fine-grained: in-slots | out-slots | done | ctl | exit flag
+  uint8_t* host = nullptr;   // pinned, fine-grained: in-slots | out-slots | done | bells | ctl | exit flag
   uint8_t* dev = nullptr;    // its device alias
-  uint64_t* d_next = nullptr;
-  uint32_t* d_exited = nullptr;
-  std::atomic<uint64_t> tail{0};
-  std::unique_ptr<std::atomic<uint64_t>[]> turn;  // per entry: the ticket allowed to use it next
+  uint8_t* d_ack = nullptr;  // device: per-entry served doorbell parity
+  uint32_t* d_exited = nullptr;  // device: {exited, quit} then the 8-B last-activity stamp
+  std::unique_ptr<std::atomic<uint32_t>[]> state;  // per entry: kFree / kBusy / kOrphan
+  std::unique_ptr<std::atomic<uint64_t>[]> pub;    // per entry: seq of its last publication
+  std::atomic<uint64_t> calls{0};                  // call numbers (seq = call + 1) and claim hints
   std::mutex launch_mu;
   std::atomic<uint64_t> running{0};  // gen of the launched kernel (0: none yet)
   uint64_t gen = 0;                  // guarded by launch_mu
   uint32_t waves = 16, idle_us = 20000, life_ms = 250;
   std::atomic<uint64_t> launches{0}, packets{0};
   int fail_launches = 0;  // test hook (WG_PP_TEST_FAIL_LAUNCHES): refuse this many launches
+  uint64_t hold_counter = ~0ull;  // test hook (WG_PP_TEST_HOLD_COUNTER / _US): a call with this counter
+  uint32_t hold_us = 0;           // sleeps between claiming its entry and publishing it
 
   uint8_t* in_slot(uint32_t i) { return host + (size_t)i * wgpp::kInSlot; }
   uint8_t* out_slot(uint32_t i) { return host + (size_t)wgpp::kRing * wgpp::kInSlot + (size_t)i * wgpp::kOutSlot; }
   size_t done_off() const { return (size_t)wgpp::kRing * (wgpp::kInSlot + wgpp::kOutSlot); }
   volatile uint64_t* done(uint32_t i) { return (volatile uint64_t*)(host + done_off()) + i; }
-  size_t ctl_off() const { return done_off() + (size_t)wgpp::kRing * 8; }
+  size_t bell_off() const { return done_off() + (size_t)wgpp::kRing * 8; }
+  uint64_t* bell(uint32_t k) { return (uint64_t*)(host + bell_off()) + k; }
+  size_t ctl_off() const { return bell_off() + (size_t)wgpp::kBells * 8; }
   volatile wgpp::Ctl* ctl() { return (volatile wgpp::Ctl*)(host + ctl_off()); }
   size_t exit_off() const { return ctl_off() + sizeof(wgpp::Ctl); }
   volatile uint64_t* exit_flag() { return (volatile uint64_t*)(host + exit_off()); }
@@ -323,8 +393,11 @@ struct PPServer {
 };
 
 void pp_free(PPServer* S) {
-  if (S->host) (void)hipHostFree(S->host);
-  if (S->d_next) (void)hipFree(S->d_next);
+  if (S->host) {
+    memset(S->host, 0, S->bytes());  // keys of entries no server took (orphans) do not outlive the ring
+    (void)hipHostFree(S->host);
+  }
+  if (S->d_ack) (void)hipFree(S->d_ack);
   if (S->d_exited) (void)hipFree(S->d_exited);
   if (S->stream) (void)hipStreamDestroy(S->stream);
 }
@@ -338,20 +411,23 @@ int pp_get(wg_ctx* c, PPServer** out) {
   DeviceGuard g(c->device);
   PPServer* S = new PPServer();
   S->c = c;
-  S->turn.reset(new std::atomic<uint64_t>[wgpp::kRing]);
-  for (uint32_t i = 0; i < wgpp::kRing; ++i) S->turn[i].store(i);
+  S->state.reset(new std::atomic<uint32_t>[wgpp::kRing]);
+  S->pub.reset(new std::atomic<uint64_t>[wgpp::kRing]);
+  for (uint32_t i = 0; i < wgpp::kRing; ++i) {
+    S->state[i].store(kFree);
+    S->pub[i].store(0);
+  }
   if (const char* e = getenv("WG_PP_TEST_FAIL_LAUNCHES")) S->fail_launches = atoi(e);
+  if (const char* e = getenv("WG_PP_TEST_HOLD_COUNTER")) S->hold_counter = strtoull(e, nullptr, 0);
+  if (const char* e = getenv("WG_PP_TEST_HOLD_US")) S->hold_us = (uint32_t)atoi(e);
   bool ok = hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking) == hipSuccess &&
             hipHostMalloc((void**)&S->host, S->bytes(), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
             hipHostGetDevicePointer((void**)&S->dev, S->host, 0) == hipSuccess &&
-            hipMalloc((void**)&S->d_next, sizeof(uint64_t) * wgpp::kMaxWaves) == hipSuccess &&
-            hipMalloc((void**)&S->d_exited, sizeof(uint32_t)) == hipSuccess;
+            hipMalloc((void**)&S->d_ack, wgpp::kRing) == hipSuccess &&
+            hipMalloc((void**)&S->d_exited, 16) == hipSuccess;
   if (ok) {
     memset(S->host, 0, S->bytes());
-    // wave w starts at ticket w (tickets t = w mod W belong to wave w)
-    uint64_t nx[wgpp::kMaxWaves];
-    for (uint32_t w = 0; w < wgpp::kMaxWaves; ++w) nx[w] = w;
-    ok = hipMemcpyAsync(S->d_next, nx, sizeof nx, hipMemcpyHostToDevice, S->stream) == hipSuccess &&
+    ok = hipMemsetAsync(S->d_ack, 0, wgpp::kRing, S->stream) == hipSuccess &&
          hipStreamSynchronize(S->stream) == hipSuccess;  // not the null stream (see wg_ctx_create)
   }
   if (!ok) {
@@ -376,10 +452,13 @@ int pp_ensure(PPServer* S) {
   P.in = S->dev;
   P.out = S->dev + (size_t)wgpp::kRing * wgpp::kInSlot;
   P.done = (uint64_t*)(S->dev + S->done_off());
+  P.bell = (const uint64_t*)(S->dev + S->bell_off());
   P.ctl = (const wgpp::Ctl*)(S->dev + S->ctl_off());
   P.exit_flag = (uint64_t*)(S->dev + S->exit_off());
-  P.next = S->d_next;
+  P.ack = S->d_ack;
   P.exited = S->d_exited;
+  P.quit = S->d_exited + 1;
+  P.last = (uint64_t*)(S->d_exited + 2);
   P.waves = S->waves;
   P.gen = (uint32_t)(S->gen + 1);
   P.idle_ticks = (uint64_t)S->idle_us * 100u;
@@ -388,7 +467,7 @@ int pp_ensure(PPServer* S) {
     --S->fail_launches;
     return fail(WG_EDEVICE, "k_pp launch refused (WG_PP_TEST_FAIL_LAUNCHES test hook)");
   }
-  HIPTRY(hipMemsetAsync(S->d_exited, 0, sizeof(uint32_t), S->stream));
+  HIPTRY(hipMemsetAsync(S->d_exited, 0, 16, S->stream));
   hipLaunchKernelGGL(wgpp::k_pp, dim3(S->waves), dim3(64), 0, S->stream, P);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(WG_EDEVICE, "k_pp launch: %s", hipGetErrorString(e));
@@ -413,6 +492,30 @@ void pp_stop(wg_ctx* c) {
   delete S;
 }
 
+// Claim a free ring entry. Calls spread over the waves (call k prefers entry (k mod W) E +
+// (k div W) mod E); any free entry will do, since every wave serves whatever is published in its
+// range. An ORPHAN entry (its caller failed after publishing) is taken over once the device has
+// completed it.
+uint32_t pp_claim(PPServer* S, uint64_t k) {
+  const uint32_t W = S->waves, E = wgpp::kRing / W;
+  const uint32_t start = (uint32_t)(k % W) * E + (uint32_t)((k / W) % E);
+  for (uint32_t spin = 0;; ++spin) {
+    for (uint32_t d = 0; d < wgpp::kRing; ++d) {
+      const uint32_t i = (start + d) % wgpp::kRing;
+      uint32_t st = S->state[i].load(std::memory_order_relaxed);
+      if (st == kOrphan && (__atomic_load_n((const uint64_t*)S->done(i), __ATOMIC_ACQUIRE) >> 8) ==
+                               S->pub[i].load(std::memory_order_relaxed)) {
+        if (S->state[i].compare_exchange_strong(st, kBusy, std::memory_order_acquire)) return i;
+      } else if (st == kFree) {
+        if (S->state[i].compare_exchange_strong(st, kBusy, std::memory_order_acquire)) return i;
+      }
+    }
+    // more calls in flight than entries: wait for one to finish
+    if (spin > 16u) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    else std::this_thread::yield();
+  }
+}
+
 // A packet longer than a slot: the host batch path with one descriptor (pageable copy
 // pipeline, device key table).
 int pp_big(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const uint8_t* src, uint32_t len, uint8_t* dst) {
@@ -433,35 +536,37 @@ int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const u
   PPServer* S;
   int rc;
   if ((rc = pp_get(c, &S)) != WG_OK) return rc;
-  // the key is read before the ticket is taken: wave t mod W serves tickets in order, so the time
-  // between taking a ticket and publishing it (no lock in it) holds up the calls behind it
   uint32_t key[8];
   {
     std::lock_guard<std::mutex> lk(c->keys_mu);
     memcpy(key, c->keys_host.data() + (size_t)key_slot * 32, 32);
   }
-  const uint64_t t = S->tail.fetch_add(1, std::memory_order_relaxed);
-  const uint32_t i = (uint32_t)(t % wgpp::kRing);
-  while (S->turn[i].load(std::memory_order_acquire) != t) std::this_thread::yield();  // ring full: wait for t - kRing
+  const uint64_t k = S->calls.fetch_add(1, std::memory_order_relaxed);
+  const uint64_t seq = k + 1;  // unique per call: the completion word echoes it
+  const uint32_t i = pp_claim(S, k);
   wgpp::Hdr* h = (wgpp::Hdr*)S->in_slot(i);
+  h->seq = seq;
   h->counter = counter;
   h->mode = open ? WG_MODE_OPEN : WG_MODE_SEAL;
   h->len = len;
   memcpy(h->key, key, 32);
   memset(key, 0, sizeof key);
   if (len || open) memcpy(S->in_slot(i) + wgpp::kHdr, src, (size_t)len + (open ? 16u : 0u));
-  __atomic_store_n(&h->seq, t + 1, __ATOMIC_RELEASE);  // publish: after every byte above
+  if (counter == S->hold_counter && S->hold_us)  // test hook: a caller descheduled before publishing
+    std::this_thread::sleep_for(std::chrono::microseconds(S->hold_us));
+  S->pub[i].store(seq, std::memory_order_relaxed);
+  // publish: toggle the entry's doorbell bit (a locked RMW, ordered after every byte above)
+  __atomic_fetch_xor(S->bell(i >> 6), 1ull << (i & 63u), __ATOMIC_SEQ_CST);
   rc = pp_ensure(S);
-  const uint64_t want = t + 1;
   uint64_t d = 0;
   for (uint64_t spin = 1; rc == WG_OK; ++spin) {
     d = __atomic_load_n((const uint64_t*)S->done(i), __ATOMIC_ACQUIRE);
-    if ((d >> 8) == want) break;
+    if ((d >> 8) == seq) break;
     // long waits (more callers than cores): sleep instead of spinning, so the callers whose results
     // have landed get a core (64 callers on 16 cores: spinning and yielding left p999 at 78 ms)
     if (spin > 4096u) std::this_thread::sleep_for(std::chrono::microseconds(spin > 8192u ? 20 : 5));
     if ((spin & 255u) == 0) {
-      rc = pp_ensure(S);  // the kernel may have exited (idle / lifetime) before taking t
+      rc = pp_ensure(S);  // the server may have left (idle / lifetime) before it saw this entry
       if (rc == WG_OK && (spin & 0xfffffu) == 0) {
         const hipError_t e = hipStreamQuery(S->stream);
         if (e != hipSuccess && e != hipErrorNotReady) rc = fail(WG_EDEVICE, "per-packet server: %s", hipGetErrorString(e));
@@ -482,11 +587,14 @@ int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const u
       result = status == WG_PKT_BADTAG ? 1 : fail(WG_EDEVICE, "per-packet server refused the packet");
     }
     S->packets.fetch_add(1, std::memory_order_relaxed);
+    memset(h->key, 0, 32);  // no key material left in the ring
+    S->state[i].store(kFree, std::memory_order_release);
+  } else {
+    // published but not served (a refused launch, a stream error): the next server serves the
+    // entry like any other (the key stays until then), and pp_claim takes it over once its
+    // completion word has landed, so the entry is never lost
+    S->state[i].store(kOrphan, std::memory_order_release);
   }
-  memset(h->key, 0, 32);  // no key material left in the ring
-  // on an error the slot stays claimed by this ticket: a late write by the device cannot
-  // reach a later packet's slot
-  if (rc == WG_OK) S->turn[i].store(t + wgpp::kRing, std::memory_order_release);
   return result;
 }
 
@@ -508,31 +616,33 @@ int wg_open1(wg_ctx* c, uint32_t key_slot, uint64_t counter, const uint8_t* in, 
   return pp_submit(c, true, key_slot, counter, in, len, pt);
 }
 
-int wg_batcher_config(wg_ctx* c, uint32_t waves, uint32_t idle_us) {
+int wg_pp_config(wg_ctx* c, uint32_t waves, uint32_t idle_us) {
   if (!c) return fail(WG_EINVAL, "NULL context");
-  if (waves == 0 || waves > wgpp::kMaxWaves) return fail(WG_EINVAL, "waves must be 1..%u", wgpp::kMaxWaves);
+  if (waves == 0 || waves > wgpp::kMaxWaves || (waves & (waves - 1u)))
+    return fail(WG_EINVAL, "waves must be a power of two in 1..%u", wgpp::kMaxWaves);
   PPServer* S;
   int rc;
   if ((rc = pp_get(c, &S)) != WG_OK) return rc;
   std::lock_guard<std::mutex> lk(S->launch_mu);
-  // the wave count fixes which wave owns which ticket: change it only between kernels
+  // the wave count fixes which wave serves which entries: change it only between kernels (the
+  // served parity is kept per entry, so no call in flight is lost across the change)
   const uint64_t g = S->running.load();
   if (g && *S->exit_flag() != g) {
     S->ctl()->stop = 1;
     (void)hipStreamSynchronize(S->stream);
     S->ctl()->stop = 0;
   }
-  if (waves != S->waves) {
-    // restart the ticket <-> wave map at the next unissued ticket (no call may be in flight)
-    const uint64_t base = S->tail.load();
-    uint64_t nx[wgpp::kMaxWaves];
-    for (uint32_t w = 0; w < wgpp::kMaxWaves; ++w) nx[w] = base + (w + waves - base % waves) % waves;
-    DeviceGuard dg(c->device);
-    HIPTRY(hipMemcpyAsync(S->d_next, nx, sizeof nx, hipMemcpyHostToDevice, S->stream));
-    HIPTRY(hipStreamSynchronize(S->stream));
-    S->waves = waves;
-  }
+  S->waves = waves;
   S->idle_us = idle_us ? idle_us : 20000;
+  return WG_OK;
+}
+
+// round-2 name and arguments (max_batch, window_us of the launch-per-batch batcher, which the
+// persistent server replaced): accepted and ignored
+int wg_batcher_config(wg_ctx* c, uint32_t max_batch, uint32_t window_us) {
+  (void)max_batch;
+  (void)window_us;
+  if (!c) return fail(WG_EINVAL, "NULL context");
   return WG_OK;
 }
 

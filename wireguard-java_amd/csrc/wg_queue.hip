@@ -1,0 +1,413 @@
+// wg_queue.hip — asynchronous batch submission, included by wg_capi.hip.
+//
+// The reference fans every packet out to the ForkJoinPool: a worker calls cipher / decipher
+// synchronously and then hands the result to the UDP / tun worker
+// (TransportManager.java:41,70-93,137-158; EstablishedSession.java:88-90). A synchronous call per
+// packet is bounded by one PCIe round trip (wg_seal1: p50 12 us), so here the producers do not
+// wait for the crypto at all:
+//   producer (an FJP worker):  wg_submit_seal / wg_submit_open copy the packet into a free slot of a
+//       pinned, device-mapped ring and push the slot id into a lock-free ready queue; they return
+//       at once (they block only when every slot is in use);
+//   dispatcher (one host thread per queue): pops ready slots into a batch, copies the batch's
+//       descriptors to the device and launches k_transport over the ring itself (zero-copy: the
+//       kernel reads the payload and writes the result over PCIe), at most `inflight` batches at a
+//       time; when a batch's event has completed it pushes the batch's slots into the completion
+//       queue. A batch is launched as soon as the device is idle, or once min_batch packets are
+//       waiting while another batch runs, so batches grow with the load and stay small (low
+//       latency) when it is light;
+//   consumer (the UDP / tun worker): wg_reap takes completions (user tag, status, a pointer to the
+//       result in the pinned ring: ct||tag for a seal, the plaintext for an open) and wg_reap_done
+//       gives their slots back after it has sent / written them.
+// Bit-exactness is that of k_transport (the same kernel as wg_seal_batch / wg_open_batch).
+#pragma once
+
+namespace wgq {
+
+// Bounded multi-producer multi-consumer queue of slot ids (Vyukov): a producer preempted inside
+// push delays the consumer by the width of one store, not by its packet copy (the copy is done
+// before the push).
+struct IdQueue {
+  struct alignas(16) Cell {
+    std::atomic<uint64_t> seq;
+    uint32_t v;
+  };
+  std::unique_ptr<Cell[]> buf;
+  uint64_t mask = 0;
+  alignas(64) std::atomic<uint64_t> head{0};
+  alignas(64) std::atomic<uint64_t> tail{0};
+
+  void init(uint32_t cap) {  // cap: a power of two
+    buf.reset(new Cell[cap]);
+    mask = cap - 1u;
+    for (uint32_t i = 0; i < cap; ++i) buf[i].seq.store(i, std::memory_order_relaxed);
+  }
+  bool push(uint32_t v) {
+    uint64_t pos = tail.load(std::memory_order_relaxed);
+    for (;;) {
+      Cell& c = buf[pos & mask];
+      const uint64_t seq = c.seq.load(std::memory_order_acquire);
+      const int64_t dif = (int64_t)seq - (int64_t)pos;
+      if (dif == 0) {
+        if (tail.compare_exchange_weak(pos, pos + 1, std::memory_order_relaxed)) {
+          c.v = v;
+          c.seq.store(pos + 1, std::memory_order_release);
+          return true;
+        }
+      } else if (dif < 0) {
+        return false;  // full
+      } else {
+        pos = tail.load(std::memory_order_relaxed);
+      }
+    }
+  }
+  bool pop(uint32_t* v) {
+    uint64_t pos = head.load(std::memory_order_relaxed);
+    for (;;) {
+      Cell& c = buf[pos & mask];
+      const uint64_t seq = c.seq.load(std::memory_order_acquire);
+      const int64_t dif = (int64_t)seq - (int64_t)(pos + 1);
+      if (dif == 0) {
+        if (head.compare_exchange_weak(pos, pos + 1, std::memory_order_relaxed)) {
+          *v = c.v;
+          c.seq.store(pos + mask + 1, std::memory_order_release);
+          return true;
+        }
+      } else if (dif < 0) {
+        return false;  // empty
+      } else {
+        pos = head.load(std::memory_order_relaxed);
+      }
+    }
+  }
+  uint64_t size_hint() const {
+    const uint64_t t = tail.load(std::memory_order_relaxed), h = head.load(std::memory_order_relaxed);
+    return t > h ? t - h : 0;
+  }
+};
+
+struct SlotMeta {  // written by the producer before the slot id is pushed
+  uint64_t user;
+  uint64_t counter;
+  uint64_t t_submit_ns;
+  uint32_t len;
+  uint32_t key_slot;
+  uint32_t status;  // set by the dispatcher when the batch completes
+  uint32_t _pad;
+};
+
+struct Batch {  // one in-flight launch
+  wg_pkt* h_desc = nullptr;    // pinned staging of its descriptors
+  wg_pkt* d_desc = nullptr;    // device copy
+  uint32_t* h_status = nullptr;  // pinned, device-mapped: open statuses (written by the kernel)
+  uint32_t* z_status = nullptr;  // its device alias
+  std::vector<uint32_t> slots;   // batch position -> ring slot
+  hipEvent_t done = nullptr;
+  uint32_t n = 0;
+};
+
+inline uint64_t now_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+}  // namespace wgq
+
+struct wg_queue {
+  wg_ctx* c = nullptr;
+  int mode = WG_MODE_SEAL;
+  uint32_t cap = 0, stride = 0, max_len = 0, max_batch = 0, min_batch = 0, inflight = 0;
+  uint8_t* h_in = nullptr;   // pinned ring: slot s at s * stride (plaintext, or ct || tag)
+  uint8_t* z_in = nullptr;   // device alias
+  uint8_t* h_out = nullptr;  // pinned ring: results (ct || tag, or plaintext)
+  uint8_t* z_out = nullptr;
+  std::unique_ptr<wgq::SlotMeta[]> meta;
+  wgq::IdQueue free_q, ready_q, done_q;
+  std::vector<wgq::Batch> batches;  // `inflight` launch buffers, used round robin
+  DevBuf lpt_hist, lpt_order;       // the queue's own longest-first workspace (its own stream)
+  hipStream_t stream = nullptr;
+  std::thread disp;
+  std::atomic<bool> quit{false};
+  std::mutex mu;                      // the two condition variables
+  std::condition_variable cv_disp, cv_reap;
+  std::atomic<int> disp_idle{0}, reapers{0};
+  std::atomic<int> err{0};
+  std::atomic<uint64_t> n_batches{0}, n_packets{0};
+};
+
+namespace {
+
+int queue_launch(wg_queue* q, wgq::Batch& b, uint32_t lmin, uint32_t lmax) {
+  wg_ctx* c = q->c;
+  HIPTRY(hipMemcpyAsync(b.d_desc, b.h_desc, sizeof(wg_pkt) * b.n, hipMemcpyHostToDevice, q->stream));
+  const uint32_t flags = lmin == lmax ? WG_F_UNIFORM : 0u;
+  const uint64_t size = (uint64_t)q->cap * q->stride;
+  int rc;
+  if (q->mode == WG_MODE_SEAL)
+    rc = launch_transport<WG_MODE_SEAL>(c, b.d_desc, b.n, q->z_in, size, q->z_out, size, nullptr, lmax, flags, q->stream,
+                                        nullptr, &q->lpt_hist, &q->lpt_order);
+  else
+    rc = launch_transport<WG_MODE_OPEN>(c, b.d_desc, b.n, q->z_in, size, q->z_out, size, b.z_status, lmax, flags,
+                                        q->stream, nullptr, &q->lpt_hist, &q->lpt_order);
+  if (rc != WG_OK) return rc;
+  HIPTRY(hipEventRecord(b.done, q->stream));
+  return WG_OK;
+}
+
+void queue_complete(wg_queue* q, wgq::Batch& b, uint32_t status_override) {
+  for (uint32_t j = 0; j < b.n; ++j) {
+    const uint32_t s = b.slots[j];
+    q->meta[s].status = status_override != 0 ? status_override
+                        : q->mode == WG_MODE_OPEN ? b.h_status[j] : (uint32_t)WG_PKT_OK;
+    while (!q->done_q.push(s)) std::this_thread::yield();  // cannot stay full: it holds at most cap ids
+  }
+  q->n_packets.fetch_add(b.n, std::memory_order_relaxed);
+  q->n_batches.fetch_add(1, std::memory_order_relaxed);
+  b.n = 0;
+  if (q->reapers.load(std::memory_order_acquire) > 0) {
+    std::lock_guard<std::mutex> lk(q->mu);
+    q->cv_reap.notify_all();
+  }
+}
+
+void queue_dispatch(wg_queue* q) {
+  DeviceGuard g(q->c->device);
+  uint32_t next = 0, oldest = 0, live = 0;  // batch ring: `live` in flight from `oldest`
+  wgq::Batch* fill = &q->batches[next];
+  uint32_t lmin = ~0u, lmax = 0;
+  while (true) {
+    // completions, oldest first
+    while (live > 0) {
+      wgq::Batch& b = q->batches[oldest];
+      const hipError_t e = hipEventQuery(b.done);
+      if (e == hipErrorNotReady) break;
+      if (e != hipSuccess) {
+        q->err.store(WG_EDEVICE);
+        fail(WG_EDEVICE, "queue batch: %s", hipGetErrorString(e));
+      }
+      queue_complete(q, b, e == hipSuccess ? 0u : (uint32_t)WG_PKT_FAILED);
+      oldest = (oldest + 1u) % q->inflight;
+      --live;
+    }
+    // gather ready packets into the batch being filled
+    if (live < q->inflight) {
+      uint32_t s;
+      while (fill->n < q->max_batch && q->ready_q.pop(&s)) {
+        const wgq::SlotMeta& m = q->meta[s];
+        wg_pkt& d = fill->h_desc[fill->n];
+        d.in_off = (uint64_t)s * q->stride;
+        d.out_off = (uint64_t)s * q->stride;
+        d.counter = m.counter;
+        d.len = m.len;
+        d.key_slot = m.key_slot;
+        fill->slots[fill->n++] = s;
+        lmin = std::min(lmin, m.len);
+        lmax = std::max(lmax, m.len);
+      }
+      // launch when the device is idle, or once min_batch packets wait while another batch runs
+      if (fill->n > 0 && (live == 0 || fill->n >= q->min_batch)) {
+        const int rc = queue_launch(q, *fill, lmin, lmax);
+        if (rc != WG_OK) {
+          q->err.store(rc);
+          queue_complete(q, *fill, WG_PKT_FAILED);
+        } else {
+          ++live;
+          next = (next + 1u) % q->inflight;
+        }
+        fill = &q->batches[next];
+        lmin = ~0u;
+        lmax = 0;
+        continue;
+      }
+    }
+    if (q->quit.load(std::memory_order_acquire) && live == 0) break;
+    if (live > 0) {
+      std::this_thread::yield();  // a batch runs: poll its event and the ready queue
+      continue;
+    }
+    // nothing in flight and nothing ready: sleep until a producer pushes (or 1 ms)
+    std::unique_lock<std::mutex> lk(q->mu);
+    q->disp_idle.store(1, std::memory_order_seq_cst);
+    if (q->ready_q.size_hint() == 0 && !q->quit.load())
+      q->cv_disp.wait_for(lk, std::chrono::milliseconds(1));
+    q->disp_idle.store(0, std::memory_order_relaxed);
+  }
+}
+
+void queue_free(wg_queue* q) {
+  for (auto& b : q->batches) {
+    if (b.h_desc) (void)hipHostFree(b.h_desc);
+    if (b.d_desc) (void)hipFree(b.d_desc);
+    if (b.h_status) (void)hipHostFree(b.h_status);
+    if (b.done) (void)hipEventDestroy(b.done);
+  }
+  if (q->h_in) (void)hipHostFree(q->h_in);
+  if (q->h_out) (void)hipHostFree(q->h_out);
+  q->lpt_hist.release();
+  q->lpt_order.release();
+  if (q->stream) (void)hipStreamDestroy(q->stream);
+}
+
+int queue_submit(wg_queue* q, int mode, uint32_t key_slot, uint64_t counter, const uint8_t* src, uint32_t len,
+                 uint64_t user) {
+  if (!q || (!src && (len || mode == WG_MODE_OPEN))) return fail(WG_EINVAL, "NULL argument");
+  if (q->mode != mode) return fail(WG_EINVAL, "a %s queue", q->mode == WG_MODE_SEAL ? "seal" : "open");
+  if (len > q->max_len) return fail(WG_E2BIG, "packet of %u bytes > the queue's max_len %u", len, q->max_len);
+  if (key_slot >= q->c->key_slots) return fail(WG_ERANGE, "key slot %u", key_slot);
+  if (const int e = q->err.load(std::memory_order_relaxed)) return fail(e, "queue failed earlier");
+  uint32_t s;
+  for (uint32_t spin = 0; !q->free_q.pop(&s); ++spin) {  // every slot in use: wait for a consumer
+    if (spin > 64u) std::this_thread::sleep_for(std::chrono::microseconds(10));
+    else std::this_thread::yield();
+  }
+  wgq::SlotMeta& m = q->meta[s];
+  m.user = user;
+  m.counter = counter;
+  m.len = len;
+  m.key_slot = key_slot;
+  m.t_submit_ns = wgq::now_ns();
+  const size_t n = (size_t)len + (mode == WG_MODE_OPEN ? 16u : 0u);
+  if (n) memcpy(q->h_in + (size_t)s * q->stride, src, n);
+  while (!q->ready_q.push(s)) std::this_thread::yield();  // holds at most cap ids: never full for long
+  if (q->disp_idle.load(std::memory_order_seq_cst)) {
+    std::lock_guard<std::mutex> lk(q->mu);
+    q->cv_disp.notify_one();
+  }
+  return WG_OK;
+}
+
+uint32_t pow2_at_least(uint32_t v) {
+  uint32_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wg_queue_create(wg_ctx* c, int mode, uint32_t capacity, uint32_t max_len, uint32_t max_batch, wg_queue** out) {
+  if (!c || !out) return fail(WG_EINVAL, "NULL argument");
+  *out = nullptr;
+  if (mode != WG_MODE_SEAL && mode != WG_MODE_OPEN) return fail(WG_EINVAL, "mode must be WG_MODE_SEAL or WG_MODE_OPEN");
+  if (max_len > WG_QUEUE_MAX_LEN) return fail(WG_E2BIG, "max_len %u > %u", max_len, WG_QUEUE_MAX_LEN);
+  if (capacity == 0) capacity = 65536;
+  if (capacity > (1u << 22)) return fail(WG_EINVAL, "capacity %u > 2^22", capacity);
+  if (max_len == 0) max_len = 2032;  // the reference pipeline's incoming limit (4-KB buffers)
+  DeviceGuard g(c->device);
+  std::unique_ptr<wg_queue> q(new wg_queue());
+  q->c = c;
+  q->mode = mode;
+  q->cap = pow2_at_least(capacity);
+  q->stride = ((max_len + 16u) + 63u) & ~63u;  // 64-B aligned slots: every payload read / store is 16-B aligned
+  q->max_len = max_len;
+  q->max_batch = std::min<uint32_t>(max_batch ? max_batch : 8192u, q->cap);
+  q->min_batch = std::max<uint32_t>(1u, std::min<uint32_t>(256u, q->max_batch / 4u));
+  q->inflight = 2;
+  q->meta.reset(new wgq::SlotMeta[q->cap]());
+  q->free_q.init(q->cap);
+  q->ready_q.init(q->cap);
+  q->done_q.init(q->cap);
+  for (uint32_t s = 0; s < q->cap; ++s) q->free_q.push(s);
+  const size_t ring = (size_t)q->cap * q->stride;
+  bool ok = hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipHostMalloc((void**)&q->h_in, ring, hipHostMallocMapped | hipHostMallocPortable) == hipSuccess &&
+            hipHostMalloc((void**)&q->h_out, ring, hipHostMallocMapped | hipHostMallocPortable) == hipSuccess;
+  if (ok) {
+    q->z_in = mapped_alias(q->h_in);
+    q->z_out = mapped_alias(q->h_out);
+    ok = q->z_in && q->z_out;
+  }
+  q->batches.resize(q->inflight);
+  for (auto& b : q->batches) {
+    if (!ok) break;
+    b.slots.resize(q->max_batch);
+    ok = hipHostMalloc((void**)&b.h_desc, sizeof(wg_pkt) * q->max_batch, hipHostMallocPortable) == hipSuccess &&
+         hipMalloc((void**)&b.d_desc, sizeof(wg_pkt) * q->max_batch) == hipSuccess &&
+         hipHostMalloc((void**)&b.h_status, sizeof(uint32_t) * q->max_batch,
+                       hipHostMallocMapped | hipHostMallocPortable) == hipSuccess &&
+         hipEventCreateWithFlags(&b.done, hipEventDisableTiming) == hipSuccess;
+    if (ok) {
+      b.z_status = (uint32_t*)mapped_alias(b.h_status);
+      ok = b.z_status != nullptr;
+    }
+  }
+  if (!ok) {
+    queue_free(q.get());
+    return fail(WG_ENOMEM, "queue: pinned rings (2 x %zu B) or device buffers could not be allocated", ring);
+  }
+  wg_queue* qp = q.release();
+  qp->disp = std::thread(queue_dispatch, qp);
+  *out = qp;
+  return WG_OK;
+}
+
+int wg_queue_destroy(wg_queue* q) {
+  if (!q) return WG_OK;
+  q->quit.store(true, std::memory_order_release);
+  {
+    std::lock_guard<std::mutex> lk(q->mu);
+    q->cv_disp.notify_all();
+  }
+  if (q->disp.joinable()) q->disp.join();  // the dispatcher leaves once nothing is in flight
+  DeviceGuard g(q->c->device);
+  (void)hipStreamSynchronize(q->stream);
+  queue_free(q);
+  delete q;
+  return WG_OK;
+}
+
+int wg_submit_seal(wg_queue* q, uint32_t key_slot, uint64_t counter, const uint8_t* pt, uint32_t len, uint64_t user) {
+  return queue_submit(q, WG_MODE_SEAL, key_slot, counter, pt, len, user);
+}
+
+int wg_submit_open(wg_queue* q, uint32_t key_slot, uint64_t counter, const uint8_t* ct_tag, uint32_t len,
+                   uint64_t user) {
+  return queue_submit(q, WG_MODE_OPEN, key_slot, counter, ct_tag, len, user);
+}
+
+int wg_reap(wg_queue* q, wg_completion* out, uint32_t max, uint32_t timeout_us) {
+  if (!q || (!out && max)) return fail(WG_EINVAL, "NULL argument");
+  uint32_t n = 0, s;
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
+  while (true) {
+    while (n < max && q->done_q.pop(&s)) {
+      const wgq::SlotMeta& m = q->meta[s];
+      wg_completion& o = out[n++];
+      o.user = m.user;
+      o.counter = m.counter;
+      o.data = q->h_out + (size_t)s * q->stride;
+      o.len = m.len;
+      o.status = m.status;
+      o.key_slot = m.key_slot;
+      o.slot = s;
+      o.submit_ns = m.t_submit_ns;
+    }
+    if (n > 0 || timeout_us == 0 || max == 0) return (int)n;
+    if (const int e = q->err.load(std::memory_order_relaxed)) return fail(e, "queue failed");
+    if (std::chrono::steady_clock::now() >= deadline) return 0;
+    std::unique_lock<std::mutex> lk(q->mu);
+    q->reapers.fetch_add(1, std::memory_order_seq_cst);
+    if (q->done_q.size_hint() == 0) q->cv_reap.wait_until(lk, std::min(deadline, std::chrono::steady_clock::now() +
+                                                                                     std::chrono::microseconds(200)));
+    q->reapers.fetch_sub(1, std::memory_order_relaxed);
+  }
+}
+
+int wg_reap_done(wg_queue* q, const wg_completion* done, uint32_t n) {
+  if (!q || (!done && n)) return fail(WG_EINVAL, "NULL argument");
+  for (uint32_t i = 0; i < n; ++i) {
+    if (done[i].slot >= q->cap) return fail(WG_EINVAL, "completion %u: slot %u", i, done[i].slot);
+    while (!q->free_q.push(done[i].slot)) std::this_thread::yield();
+  }
+  return WG_OK;
+}
+
+int wg_queue_stats(wg_queue* q, uint64_t* batches, uint64_t* packets) {
+  if (!q) return fail(WG_EINVAL, "NULL queue");
+  if (batches) *batches = q->n_batches.load();
+  if (packets) *packets = q->n_packets.load();
+  return WG_OK;
+}
+
+}  // extern "C"

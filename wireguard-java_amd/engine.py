@@ -285,6 +285,10 @@ class Engine:
                                        out.ctypes.data, out_size, status.ctypes.data))
         return out[:out_size].tobytes(), status
 
+    def queue(self, mode: str, capacity: int = 0, max_len: int = 0, max_batch: int = 0) -> "Queue":
+        """wg_queue_create: an asynchronous seal ("seal") or open ("open") queue on this context."""
+        return Queue(self, mode, capacity, max_len, max_batch)
+
     def seal1(self, slot: int, counter: int, pt: bytes) -> bytes:
         src = np.frombuffer(pt, np.uint8).copy() if pt else np.zeros(1, np.uint8)
         out = np.zeros(len(pt) + 16, np.uint8)
@@ -298,10 +302,12 @@ class Engine:
         rc = L.check(self._lib.wg_open1(self.ctx, slot, counter, src.ctypes.data, n, out.ctypes.data))
         return None if rc == 1 else out[:n].tobytes()
 
-    def batcher_config(self, waves: int = 16, idle_us: int = 20000) -> None:
-        """wg_batcher_config: waves of the persistent per-packet server (k_pp) that serves
-        seal1/open1, and how long it stays resident without work (microseconds)."""
-        L.check(self._lib.wg_batcher_config(self.ctx, waves, idle_us))
+    def pp_config(self, waves: int = 16, idle_us: int = 20000) -> None:
+        """wg_pp_config: waves of the persistent per-packet server (k_pp) that serves
+        seal1/open1 (a power of two), and how long it stays resident without work (microseconds)."""
+        L.check(self._lib.wg_pp_config(self.ctx, waves, idle_us))
+
+    batcher_config = pp_config  # round-3 name
 
     def batcher_stats(self) -> tuple[int, int]:
         """(server launches, packets served) of the per-packet path so far."""
@@ -350,3 +356,52 @@ def _host_buf(x):
         assert x.flags.c_contiguous
         return x.ctypes.data, x.nbytes
     return x.data_ptr(), x.numel() * x.element_size()
+
+
+class Queue:
+    """wg_queue: producers submit packets without waiting for the crypto (wg_submit_seal /
+    wg_submit_open), a consumer reaps the results (wg_reap, wg_reap_done). The batching
+    replacement for TransportManager's per-packet ForkJoinPool submission
+    (TransportManager.java:41,70-93,137-158)."""
+
+    def __init__(self, engine: Engine, mode: str, capacity: int = 0, max_len: int = 0, max_batch: int = 0):
+        self._lib = engine._lib
+        self.mode = {"seal": L.WG_MODE_SEAL, "open": L.WG_MODE_OPEN}[mode]
+        q = ctypes.c_void_p()
+        L.check(self._lib.wg_queue_create(engine.ctx, self.mode, capacity, max_len, max_batch, ctypes.byref(q)))
+        self.q = q.value
+        self._buf = (L.WgCompletion * 4096)()
+
+    def submit(self, key_slot: int, counter: int, data: bytes, user: int = 0) -> None:
+        """seal: data = plaintext; open: data = ct || tag."""
+        n = len(data) - (16 if self.mode == L.WG_MODE_OPEN else 0)
+        if n < 0:
+            raise ValueError("open needs ct || tag (at least 16 bytes)")
+        src = np.frombuffer(bytes(data), np.uint8) if data else np.zeros(1, np.uint8)
+        fn = self._lib.wg_submit_seal if self.mode == L.WG_MODE_SEAL else self._lib.wg_submit_open
+        L.check(fn(self.q, key_slot, counter, src.ctypes.data, n, user))
+
+    def reap(self, max_n: int = 4096, timeout_us: int = 100000):
+        """[(user, counter, status, result bytes)], the slots handed back at once; the result is
+        ct || tag for a seal, the plaintext for an open (None unless status is WG_PKT_OK)."""
+        m = min(max_n, len(self._buf))
+        n = L.check(self._lib.wg_reap(self.q, self._buf, m, timeout_us))
+        out = []
+        for k in range(n):
+            c = self._buf[k]
+            size = c.len + (16 if self.mode == L.WG_MODE_SEAL else 0)
+            ok = c.status == L.WG_PKT_OK
+            data = ctypes.string_at(c.data, size) if ok and size else (b"" if ok else None)
+            out.append((c.user, c.counter, c.status, data))
+        L.check(self._lib.wg_reap_done(self.q, self._buf, n))
+        return out
+
+    def stats(self) -> tuple[int, int]:
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        L.check(self._lib.wg_queue_stats(self.q, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    def close(self) -> None:
+        if self.q:
+            L.check(self._lib.wg_queue_destroy(self.q))
+            self.q = None
