@@ -343,6 +343,10 @@ def main():
     ap.add_argument("--kernel", default="default", help="transport kernel (wg_ctx_set_kernel): default|wave1|tile")
     # --variant 1: a WG_F_AFTER_SEAL step as two launches (seal, then open) instead of one k_step launch
     ap.add_argument("--variant", type=int, default=0, choices=[0, 1])
+    # --graph: the K timed steps are captured once into a HIP graph (torch.cuda.CUDAGraph) and the timed
+    # region is one replay of it: the same launches with no host enqueue between them (used for the
+    # kernel traces, where the profiler makes each host enqueue slower than a step)
+    ap.add_argument("--graph", action="store_true")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     # diagnostic knobs (not the metric's configuration): batch size and session count of C1 / C2
     ap.add_argument("--packets", type=int, default=0, help=argparse.SUPPRESS)
@@ -457,13 +461,26 @@ def main():
     # HIP events on the stream the kernels are launched on (torch's current stream,
     # which Engine passes to wg_seal_batch / wg_open_batch), around the whole region
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    graph = None
+    if args.graph:
+        if K != 1 or args.mode == "duplex":
+            raise SystemExit("--graph captures one stream of step launches (--streams 1, --mode step|serial)")
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for _ in range(args.steps):
+                step()
+        graph.replay()  # warm: the graph's first launch
+        torch.cuda.synchronize()
     if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record()
-    for _ in range(args.steps):
-        step()
+    if graph is not None:
+        graph.replay()
+    else:
+        for _ in range(args.steps):
+            step()
     t_enq = time.perf_counter()  # host time to enqueue the steps (the GPU idles if it is ~ ms_per_step)
     ev1.record()
     torch.cuda.synchronize()
@@ -577,6 +594,8 @@ def main():
             "ramp_steps": ramp_steps,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
             "host_enqueue_ms_per_step": round((t_enq - t0) * 1e3 / args.steps, 4),
+            "graph": bool(args.graph),
+            "graph_warm_steps": args.steps if args.graph else 0,  # the graph's warm replay, before the timed one
             "higher_is_better": True,
             "scaling": "strong" if args.workload == "c3" else "weak",
             "vs_baseline": None,

@@ -236,6 +236,48 @@ def test_in_place_open_keeps_forged_packets(engine, shift, uniform):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("kernel", ["tile", "wave1"])
+def test_other_kernels_in_place_open_and_rx_filter(kernel):
+    """with wg_ctx_set_kernel("tile" / "wave1") an open whose buffers overlap still runs
+    the verify-first transport kernel (a forged packet's bytes stay as they were, as every kernel
+    must write identical bytes), and WG_F_RX_FILTER is refused (WG_EINVAL) instead of silently
+    skipping the AllowedIPs verdict."""
+    torch, dev = _dev()
+    W = wg()
+    eng = W.Engine(0, key_slots=2)
+    try:
+        eng.set_kernel(kernel)
+        n, L = 24, 700
+        S = ((L + 16 + 15) // 16) * 16
+        off = np.arange(n, dtype=np.uint64) * S
+        keys = splitmix_np(81, 32)
+        pt = splitmix_np(82, n * S)
+        sd = W.pack_desc(off, off, np.arange(n, dtype=np.uint64), L, 0)
+        sealed = pt.copy()
+        O.seal_batch(sd, pt, sealed, keys, threads=1)
+        forged = np.arange(n) % 5 == 2
+        for i in np.nonzero(forged)[0]:
+            sealed[int(off[i]) + L] ^= 1
+        eng.set_keys(0, keys.tobytes())
+        buf = torch.from_numpy(sealed.copy()).to(dev)
+        st = torch.zeros(n, dtype=torch.int32, device=dev)
+        d = torch.from_numpy(W.desc_as_int64(sd)).to(dev)
+        eng.open(d, buf, buf, st, L, uniform=True)
+        torch.cuda.synchronize()
+        assert st.cpu().numpy().tolist() == forged.astype(np.int32).tolist()
+        got = buf.cpu().numpy()
+        for i in range(n):
+            o = int(off[i])
+            want = sealed[o:o + L + 16] if forged[i] else np.concatenate([pt[o:o + L], sealed[o + L:o + L + 16]])
+            assert np.array_equal(got[o:o + L + 16], want), (i, bool(forged[i]))
+        out = torch.zeros_like(buf)
+        with pytest.raises(W.WgError) as e:
+            eng.open(d, buf, out, st, L, uniform=True, rx_filter=True)
+        assert e.value.code == W._lib.WG_EINVAL
+    finally:
+        eng.close()
+
+
 def test_batch_argument_contract(engine):
     """open needs a status array; unknown flag bits and WG_F_FRAME on open are
     refused (WG_EINVAL) instead of silently ignored."""

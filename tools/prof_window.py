@@ -34,7 +34,7 @@ def bench_line(path):
 
 def window(b):
     per = b["roofline"].get("launches_per_step", 1)
-    skip = (b["ramp_steps"] + b["warmup"]) * per
+    skip = (b["ramp_steps"] + b["warmup"] + b.get("graph_warm_steps", 0)) * per
     return skip, b["steps"] * per, per
 
 
@@ -68,7 +68,8 @@ def trace(args):
     busy_us = sum(sum(v) for v in per_kernel.values())
     out = {
         "source": f"rocprofv3 --kernel-trace of the bench command; dispatches {skip}..{skip + take - 1} of {sorted(want)} "
-                  f"(ramp {b['ramp_steps']} + warmup {b['warmup']} steps skipped, {b['steps']} timed steps x {per})",
+                  f"(ramp {b['ramp_steps']} + warmup {b['warmup']} + graph warm {b.get('graph_warm_steps', 0)} steps "
+                  f"skipped, {b['steps']} timed steps x {per}{', one graph replay' if b.get('graph') else ''})",
         "bench_ms_per_step": b["ms_per_step"],
         "bench_frac": b["roofline"]["frac"],
         "window_span_us": round(span_us, 2),

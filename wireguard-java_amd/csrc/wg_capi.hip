@@ -419,12 +419,18 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
   if (!desc || (((uintptr_t)desc) & 15u)) return fail(WG_EINVAL, "descriptor array must be non-NULL and 16-byte aligned");
   if (!in || !out) return fail(WG_EINVAL, "NULL buffer");
   if (max_len > WG_MAX_PACKET) return fail(WG_E2BIG, "max_len %u > WG_MAX_PACKET", max_len);
+  // an open whose buffers overlap runs the transport kernel whatever kernel is selected: only its
+  // verify-first variant leaves a forged in-place packet's bytes untouched (ChaCha20Poly1305.java:40-56),
+  // and every selectable kernel must write identical bytes (include/wgaead.h)
+  int kern = c->kern;
+  if (MODE == WG_MODE_OPEN && kern != KERN_TRANSPORT && open_overlaps(in, in_size, out, out_size)) kern = KERN_TRANSPORT;
+  if (rx && kern != KERN_TRANSPORT) return fail(WG_EINVAL, "WG_F_RX_FILTER needs the transport kernel");
   // k_tile's uniform plan sizes every tile for max_len-long packets; WG_F_UNIFORM is only a
   // scheduling hint of the transport API, so the tile kernel always plans from the lengths
-  if (c->kern == KERN_TILE)
+  if (kern == KERN_TILE)
     return launch_tiles<MODE, false>(c, desc, n, in, in_size, nullptr, 0, out, out_size, status, max_len,
                                      flags & ~WG_F_UNIFORM, s);
-  if (c->kern == KERN_WAVE1) {
+  if (kern == KERN_WAVE1) {
     wgk::StreamParams P{};
     P.desc = desc;
     P.n = n;
@@ -451,7 +457,6 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
   const SlotPlan sp = slot_plan(c, flags, n);
   const uint32_t G = sp.G;
   const uint64_t cap_waves = std::max<uint32_t>(c->resident_waves[G == 16][MODE == WG_MODE_OPEN], wgt::TW);
-  if (rx && c->kern != KERN_TRANSPORT) return fail(WG_EINVAL, "WG_F_RX_FILTER needs the transport kernel");
   const bool own = own_hist && own_order;  // the caller holds the plan workspace (launch_after_seal)
   int rc = plan_transport<MODE>(c, desc, n, in, in_size, out, out_size, status, max_len, flags, s, cap_waves, G,
                                 own ? *own_hist : c->lpt_hist, own ? *own_order : c->lpt_order, &P, &grid, &ordered,

@@ -565,6 +565,10 @@ int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const u
     // long waits (more callers than cores): sleep instead of spinning, so the callers whose results
     // have landed get a core (64 callers on 16 cores: spinning and yielding left p999 at 78 ms)
     if (spin > 4096u) std::this_thread::sleep_for(std::chrono::microseconds(spin > 8192u ? 20 : 5));
+    if (spin == (1u << 20) && getenv("WG_PP_DEBUG"))  // a call waiting for seconds: say why
+      fprintf(stderr, "[wg_pp] entry %u seq %llu waits: done %llx bell %llx running %llu exit_flag %llu waves %u\n", i,
+              (unsigned long long)seq, (unsigned long long)d, (unsigned long long)*S->bell(i >> 6),
+              (unsigned long long)S->running.load(), (unsigned long long)*S->exit_flag(), S->waves);
     if ((spin & 255u) == 0) {
       rc = pp_ensure(S);  // the server may have left (idle / lifetime) before it saw this entry
       if (rc == WG_OK && (spin & 0xfffffu) == 0) {

@@ -37,7 +37,8 @@ public final class WgAead {
 
 	static final MethodHandle SELFTEST, CTX_CREATE, LAST_ERROR, KEYS_SET, KEYS_ZERO, SEAL1, OPEN1, AEAD_HOST,
 		SEAL_BATCH, OPEN_BATCH, SYNC, SEAL_HOST, OPEN_HOST, HOST_ALLOC, HOST_FREE, FRAME_SEAL, PARSE_OPEN,
-		FILTER_SET, SLOT_FILTERS_SET, REPLAY_ENABLE, REPLAY_RESET, RX_CHECK, DUPLEX_BATCH;
+		FILTER_SET, SLOT_FILTERS_SET, REPLAY_ENABLE, REPLAY_RESET, RX_CHECK, DUPLEX_BATCH, QUEUE_CREATE,
+		QUEUE_DESTROY, SUBMIT_SEAL, SUBMIT_OPEN, REAP, REAP_DONE;
 
 	/** The process-wide context (one HIP device, its stream and its device key table). */
 	static final MemorySegment CTX;
@@ -88,6 +89,17 @@ public final class WgAead {
 		// outgoing seal + incoming open in one launch (two wg_batch structs of 64 bytes)
 		DUPLEX_BATCH = down(linker, symbols, "wg_duplex_batch", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, ADDRESS,
 			ADDRESS));
+
+		// asynchronous batch submission (TransportQueue: TransportManager.java:41,70-93,137-158)
+		QUEUE_CREATE = down(linker, symbols, "wg_queue_create", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT,
+			JAVA_INT, JAVA_INT, JAVA_INT, ADDRESS));
+		QUEUE_DESTROY = down(linker, symbols, "wg_queue_destroy", FunctionDescriptor.of(JAVA_INT, ADDRESS));
+		SUBMIT_SEAL = down(linker, symbols, "wg_submit_seal", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT,
+			JAVA_LONG, ADDRESS, JAVA_INT, JAVA_LONG));
+		SUBMIT_OPEN = down(linker, symbols, "wg_submit_open", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT,
+			JAVA_LONG, ADDRESS, JAVA_INT, JAVA_LONG));
+		REAP = down(linker, symbols, "wg_reap", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT, JAVA_INT));
+		REAP_DONE = down(linker, symbols, "wg_reap_done", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT));
 
 		int device = Integer.getInteger("wg.device", 0);
 		KEY_SLOTS = Integer.getInteger("wg.keySlots", 65536);
