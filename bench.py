@@ -418,6 +418,14 @@ def main():
     def step():
         if args.mode == "duplex":
             return step_duplex()
+        if K == 1:  # the current stream (a graph's capture stream under --graph)
+            if args.mode == "step":
+                eng.duplex(d_desc, pt, ct, max_len, d_desc, ct, back, status, max_len, uniform=uniform,
+                           after_seal=True)
+            else:
+                eng.seal(d_desc, pt, ct, max_len, uniform=uniform)
+                eng.open(d_desc, ct, back, status, max_len, uniform=uniform)
+            return
         if args.mode == "step":
             for i in range(K):
                 a, b = cuts[i], cuts[i + 1]

@@ -234,6 +234,18 @@ def _batcher_bench(*args, timeout=120):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("waves", [1, 4, 8, 16, 64])
+def test_every_wave_count_serves_every_entry(waves):
+    """wg_pp_config with each power-of-two wave count (a wave owns 512 / waves ring entries: 512 in
+    8 doorbell words down to 8 in a sub-word) and a 200-us idle timeout (the server leaves and is
+    relaunched between bursts): 4 threads x 600 calls reach every entry, including doorbell bits
+    31 and 32 (a sign-extension bug in the 64-bit doorbell handling once lost every entry past
+    bit 31 of a wave's word)."""
+    j = _batcher_bench(4, 600, 0, f"waves={waves}", "idle_us=200")
+    assert j["failures"] == 0 and j["calls"] == 2400, j
+
+
+@pytest.mark.gpu
 def test_held_caller_delays_nobody():
     """One caller is held 50 ms between claiming its ring entry and publishing it (a caller
     descheduled mid-call, test hook WG_PP_TEST_HOLD_*) while 16 others run: with out-of-order

@@ -10,6 +10,7 @@ import json
 import os
 import subprocess
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -31,25 +32,32 @@ def test_queue_seal_then_open_bit_exact():
         qs, qo = eng.queue("seal", capacity=4096), eng.queue("open", capacity=4096)
         T, N = 4, 3000
         sent = {}
+        errors = []
         lock = threading.Lock()
 
         def producer(t):
-            rng = np.random.default_rng(t)
-            for i in range(N):
-                L = int(rng.integers(0, 2033)) if i % 7 else (0 if i % 2 else 2032)
-                user = (t << 32) | i
-                pt = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
-                with lock:
-                    sent[user] = (i % 16, (t << 40) | i, pt)
-                qs.submit(i % 16, (t << 40) | i, pt, user)
+            try:
+                rng = np.random.default_rng(t)
+                for i in range(N):
+                    L = int(rng.integers(0, 2033)) if i % 7 else (0 if i % 2 else 2032)
+                    user = (t << 32) | i
+                    pt = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+                    with lock:
+                        sent[user] = (i % 16, (t << 40) | i, pt)
+                    qs.submit(i % 16, (t << 40) | i, pt, user)
+            except Exception as e:  # pragma: no cover - reported by the reaping loop
+                errors.append(repr(e))
 
-        th = [threading.Thread(target=producer, args=(t,)) for t in range(T)]
+        th = [threading.Thread(target=producer, args=(t,), daemon=True) for t in range(T)]
         for x in th:
             x.start()
         sealed = {}
+        deadline = time.monotonic() + 60
         while len(sealed) < T * N:
+            assert not errors, errors[:3]
+            assert time.monotonic() < deadline, (len(sealed), qs.stats())
             for user, ctr, st, data in qs.reap(4096, 200000):
-                assert st == 0
+                assert st == 0, st
                 sealed[user] = (ctr, data)
         for x in th:
             x.join()
@@ -58,18 +66,32 @@ def test_queue_seal_then_open_bit_exact():
             key = keys[32 * slot:32 * slot + 32].tobytes()
             assert sealed[user][0] == ctr
             assert sealed[user][1] == O.c_aead_seal(key, O.transport_nonce(ctr), pt), user
-        # the peer's side: open every packet, about 2% with a flipped tag bit
+        # the peer's side: open every packet, about 2% with a flipped tag bit; the main thread
+        # submits (more packets than the queue has slots) while a consumer thread reaps
         forged = set()
+        got = {}
+        stop = threading.Event()
+
+        def consumer():
+            try:
+                while not stop.is_set() and len(got) < T * N:
+                    for user, ctr, st, data in qo.reap(4096, 20000):
+                        got[user] = (st, data)
+            except Exception as e:  # pragma: no cover - reported below
+                errors.append(repr(e))
+
+        rc = threading.Thread(target=consumer, daemon=True)
+        rc.start()
         for k, (user, (slot, ctr, pt)) in enumerate(sorted(sent.items())):
             ct = bytearray(sealed[user][1])
             if k % 50 == 7:
                 ct[len(pt) + (k % 16)] ^= 0x04
                 forged.add(user)
             qo.submit(slot, ctr, bytes(ct), user)
-        got = {}
-        while len(got) < T * N:
-            for user, ctr, st, data in qo.reap(4096, 200000):
-                got[user] = (st, data)
+        rc.join(timeout=60)
+        stop.set()
+        assert not errors, errors[:3]
+        assert len(got) == T * N, (len(got), qo.stats())
         for user, (slot, ctr, pt) in sent.items():
             st, data = got[user]
             if user in forged:

@@ -7,7 +7,7 @@
  *
  * Build: make -C tools queue_bench
  * Run:   tools/queue_bench [producers=16] [packets_per_producer=200000] [len=1420|0 mixed 64..1500]
- *                          [max_batch=8192]
+ *                          [max_batch=8192] [forwarders=1] [verifiers=1]
  * Output: one JSON line: seal+open payload GiB/s over the whole run (both directions' payload bytes,
  * as bench.py's cpu_baseline counts them), seal-side rate, latency percentiles per queue (submit ->
  * reap), batches per queue. Exit status 1 on any failed status or byte mismatch. */
@@ -149,6 +149,7 @@ int main(int argc, char** argv) {
   g_N = argc > 2 ? atoi(argv[2]) : 200000;
   g_len = argc > 3 ? atoi(argv[3]) : 1420;
   const int max_batch = argc > 4 ? atoi(argv[4]) : 8192;
+  const int nf = argc > 5 ? atoi(argv[5]) : 1, nv = argc > 6 ? atoi(argv[6]) : 1;
   if (g_P < 1 || g_P > 256 || g_N < 1 || g_len < 0 || g_len > 1500) {
     fprintf(stderr, "usage: queue_bench [producers] [packets_per_producer] [len 0..1500] [max_batch]\n");
     return 2;
@@ -179,16 +180,20 @@ int main(int argc, char** argv) {
   for (int t = 0; t < g_P; ++t)
     for (int i = 0; i < g_N; ++i) bytes += pkt_len(((uint64_t)t << 40) | (uint64_t)i);
 
-  pthread_t th[258];
+  if (nf < 1 || nf > 8 || nv < 1 || nv > 8) {
+    fprintf(stderr, "forwarders / verifiers: 1..8\n");
+    return 2;
+  }
+  pthread_t th[256 + 16];
   const uint64_t t0 = now_ns();
-  pthread_create(&th[g_P], NULL, forwarder, NULL);
-  pthread_create(&th[g_P + 1], NULL, verifier, NULL);
+  for (int k = 0; k < nf; ++k) pthread_create(&th[g_P + k], NULL, forwarder, NULL);
+  for (int k = 0; k < nv; ++k) pthread_create(&th[g_P + nf + k], NULL, verifier, NULL);
   for (int t = 0; t < g_P; ++t) pthread_create(&th[t], NULL, producer, (void*)(intptr_t)t);
   for (int t = 0; t < g_P; ++t) pthread_join(th[t], NULL);
   const double t_submit = (now_ns() - t0) * 1e-9;
-  pthread_join(th[g_P], NULL);
+  for (int k = 0; k < nf; ++k) pthread_join(th[g_P + k], NULL);
   const double t_sealed = (now_ns() - t0) * 1e-9;
-  pthread_join(th[g_P + 1], NULL);
+  for (int k = 0; k < nv; ++k) pthread_join(th[g_P + nf + k], NULL);
   const double wall = (now_ns() - t0) * 1e-9;
   uint64_t bs = 0, ps = 0, bo = 0, po = 0;
   wg_queue_stats(g_qs, &bs, &ps);
@@ -198,13 +203,13 @@ int main(int argc, char** argv) {
   pct(g_lat_s, ns, ls);
   pct(g_lat_o, no, lo);
   const double gib = (double)(1u << 30);
-  printf("{\"tool\": \"queue_bench\", \"producers\": %d, \"packets\": %llu, \"len\": \"%s\", \"max_batch\": %d, "
+  printf("{\"tool\": \"queue_bench\", \"producers\": %d, \"forwarders\": %d, \"verifiers\": %d, \"packets\": %llu, \"len\": \"%s\", \"max_batch\": %d, "
          "\"bad\": %llu, \"wall_s\": %.4f, \"seal_open_gib_s\": %.3f, \"seal_gib_s\": %.3f, "
          "\"submit_gib_s\": %.3f, \"packets_per_s\": %.0f, "
          "\"seal_lat_us\": {\"p50\": %.1f, \"p99\": %.1f, \"p999\": %.1f, \"max\": %.1f}, "
          "\"open_lat_us\": {\"p50\": %.1f, \"p99\": %.1f, \"p999\": %.1f, \"max\": %.1f}, "
          "\"seal_batches\": %llu, \"seal_mean_batch\": %.1f, \"open_batches\": %llu, \"open_mean_batch\": %.1f}\n",
-         g_P, (unsigned long long)g_total, g_len ? argv[3] : "mixed 64..1500", max_batch,
+         g_P, nf, nv, (unsigned long long)g_total, g_len ? argv[3] : "mixed 64..1500", max_batch,
          (unsigned long long)g_bad, wall, 2.0 * bytes / wall / gib, bytes / t_sealed / gib, bytes / t_submit / gib,
          g_total / wall, ls[0], ls[1], ls[2], ls[3], lo[0], lo[1], lo[2], lo[3], (unsigned long long)bs,
          bs ? (double)ps / bs : 0.0, (unsigned long long)bo, bo ? (double)po / bo : 0.0);

@@ -246,6 +246,14 @@ __device__ void pp_packet(const Hdr& h, uint64_t ticket, const uint8_t* slot, ui
     __hip_atomic_store(done, (ticket << 8) | status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// lane k's 64-bit value (k wave-uniform). readlane returns int: each half goes through uint32_t, or
+// a low half with bit 31 set would sign-extend over the high half when the two are combined
+__device__ __forceinline__ uint64_t lane_u64(uint64_t v, uint32_t k) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)k);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)k);
+  return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ uint64_t ld_agent64(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -285,8 +293,7 @@ __global__ void __launch_bounds__(64) k_pp(PPParams P) {
     if (__any(pend != 0)) {
       // serve every entry pending in this snapshot, in index order
       for (uint32_t k = 0; k < nwords; ++k) {
-        uint64_t pk = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(pend >> 32), k) << 32) |
-                      __builtin_amdgcn_readlane((uint32_t)pend, k);
+        uint64_t pk = lane_u64(pend, k);
         while (pk) {
           const uint32_t bit = (uint32_t)__builtin_ctzll(pk);
           pk &= pk - 1ull;
@@ -307,8 +314,7 @@ __global__ void __launch_bounds__(64) k_pp(PPParams P) {
           Hdr h = *(const Hdr*)raw;
           h.mode = __builtin_amdgcn_readfirstlane(h.mode);
           h.len = __builtin_amdgcn_readfirstlane(h.len);
-          const uint64_t seq = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(h.seq >> 32)) << 32) |
-                               __builtin_amdgcn_readfirstlane((uint32_t)h.seq);
+          const uint64_t seq = lane_u64(h.seq, 0);  // every lane read the same header
 #ifdef WG_PP_STAMPS
           if (lane == 0) g_pp_stamps[seq % 4096u][0] = t_seen;
 #endif
@@ -341,8 +347,7 @@ __global__ void __launch_bounds__(64) k_pp(PPParams P) {
   }
   // this wave's acknowledged parity back to the per-entry bytes, for the next launch
   for (uint32_t k = 0; k < nwords; ++k) {
-    const uint64_t a = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(ack >> 32), k) << 32) |
-                       __builtin_amdgcn_readlane((uint32_t)ack, k);
+    const uint64_t a = lane_u64(ack, k);
     const uint32_t e = 64u * (word0 + k) + lane;
     if (e >= base && e < base + E) P.ack[e] = (uint8_t)((a >> lane) & 1ull);
   }
@@ -510,6 +515,17 @@ uint32_t pp_claim(PPServer* S, uint64_t k) {
         if (S->state[i].compare_exchange_strong(st, kBusy, std::memory_order_acquire)) return i;
       }
     }
+    if (spin == 20000u && getenv("WG_PP_DEBUG")) {
+      uint32_t nf = 0, nb = 0, no = 0;
+      for (uint32_t i = 0; i < wgpp::kRing; ++i) {
+        const uint32_t st = S->state[i].load();
+        nf += st == kFree;
+        nb += st == kBusy;
+        no += st == kOrphan;
+      }
+      fprintf(stderr, "[wg_pp] claim of call %llu finds no free entry: free %u busy %u orphan %u\n",
+              (unsigned long long)k, nf, nb, no);
+    }
     // more calls in flight than entries: wait for one to finish
     if (spin > 16u) std::this_thread::sleep_for(std::chrono::microseconds(20));
     else std::this_thread::yield();
@@ -565,7 +581,7 @@ int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const u
     // long waits (more callers than cores): sleep instead of spinning, so the callers whose results
     // have landed get a core (64 callers on 16 cores: spinning and yielding left p999 at 78 ms)
     if (spin > 4096u) std::this_thread::sleep_for(std::chrono::microseconds(spin > 8192u ? 20 : 5));
-    if (spin == (1u << 20) && getenv("WG_PP_DEBUG"))  // a call waiting for seconds: say why
+    if (spin == 100000u && getenv("WG_PP_DEBUG"))  // a call waiting for a second or more: say why
       fprintf(stderr, "[wg_pp] entry %u seq %llu waits: done %llx bell %llx running %llu exit_flag %llu waves %u\n", i,
               (unsigned long long)seq, (unsigned long long)d, (unsigned long long)*S->bell(i >> 6),
               (unsigned long long)S->running.load(), (unsigned long long)*S->exit_flag(), S->waves);

@@ -6,15 +6,15 @@
 // packet is bounded by one PCIe round trip (wg_seal1: p50 12 us), so here the producers do not
 // wait for the crypto at all:
 //   producer (an FJP worker):  wg_submit_seal / wg_submit_open copy the packet into a free slot of a
-//       pinned, device-mapped ring and push the slot id into a lock-free ready queue; they return
-//       at once (they block only when every slot is in use);
-//   dispatcher (one host thread per queue): pops ready slots into a batch, copies the batch's
-//       descriptors to the device and launches k_transport over the ring itself (zero-copy: the
-//       kernel reads the payload and writes the result over PCIe), at most `inflight` batches at a
+//       pinned, device-mapped ring and append the slot to its lane's ready ring (per-thread lanes,
+//       so producers share no cache line); they return at once (they block only when every slot of
+//       their lane is in use);
+//   dispatcher (one host thread per queue): pops ready slots into a batch, writes its descriptors
+//       into pinned memory and launches k_transport over the ring itself (zero-copy: the kernel
+//       reads descriptors and payload and writes the result over PCIe), at most `inflight` batches at a
 //       time; when a batch's event has completed it pushes the batch's slots into the completion
-//       queue. A batch is launched as soon as the device is idle, or once min_batch packets are
-//       waiting while another batch runs, so batches grow with the load and stay small (low
-//       latency) when it is light;
+//       queue. A batch is launched once min_batch (512) packets wait, or when its first packet has
+//       waited 20 us, so batches grow with the load and a light load waits at most 20 us;
 //   consumer (the UDP / tun worker): wg_reap takes completions (user tag, status, a pointer to the
 //       result in the pinned ring: ct||tag for a seal, the plaintext for an open) and wg_reap_done
 //       gives their slots back after it has sent / written them.
@@ -85,6 +85,34 @@ struct IdQueue {
   }
 };
 
+// Producers submit through lanes, so they never share a cache line with each other: a thread takes
+// lane (thread number mod lanes) of a queue, and a lane owns the ring slots [lane K, (lane + 1) K).
+// Its free list (slots the consumers handed back) and its ready list (slots filled and waiting for
+// the dispatcher) are single-producer / single-consumer rings; the lane lock is only contended when
+// two threads map to one lane, the free lock only among consumer threads.
+struct Lane {
+  alignas(64) std::atomic<uint32_t> lock{0};  // the lane's producer(s)
+  alignas(64) std::atomic<uint64_t> r_tail{0};  // ready ring: pushed under `lock`
+  alignas(64) std::atomic<uint64_t> r_head{0};  // popped by the dispatcher alone
+  alignas(64) std::atomic<uint32_t> flock{0};   // free ring pushes (consumers)
+  std::atomic<uint64_t> f_tail{0};
+  alignas(64) std::atomic<uint64_t> f_head{0};  // free ring pops: under `lock`
+  std::unique_ptr<uint32_t[]> ready, freel;     // K entries each
+};
+
+inline void spin_lock(std::atomic<uint32_t>& l) {
+  for (uint32_t k = 0; l.exchange(1, std::memory_order_acquire); ++k)
+    if (k > 64) std::this_thread::yield();
+    else __builtin_ia32_pause();
+}
+inline void spin_unlock(std::atomic<uint32_t>& l) { l.store(0, std::memory_order_release); }
+
+inline uint32_t thread_number() {
+  static std::atomic<uint32_t> next{0};
+  thread_local uint32_t id = next.fetch_add(1, std::memory_order_relaxed);
+  return id;
+}
+
 struct SlotMeta {  // written by the producer before the slot id is pushed
   uint64_t user;
   uint64_t counter;
@@ -96,8 +124,8 @@ struct SlotMeta {  // written by the producer before the slot id is pushed
 };
 
 struct Batch {  // one in-flight launch
-  wg_pkt* h_desc = nullptr;    // pinned staging of its descriptors
-  wg_pkt* d_desc = nullptr;    // device copy
+  wg_pkt* h_desc = nullptr;    // pinned, device-mapped: its descriptors
+  wg_pkt* z_desc = nullptr;    // their device alias (the kernel reads them over PCIe)
   uint32_t* h_status = nullptr;  // pinned, device-mapped: open statuses (written by the kernel)
   uint32_t* z_status = nullptr;  // its device alias
   std::vector<uint32_t> slots;   // batch position -> ring slot
@@ -117,12 +145,16 @@ struct wg_queue {
   wg_ctx* c = nullptr;
   int mode = WG_MODE_SEAL;
   uint32_t cap = 0, stride = 0, max_len = 0, max_batch = 0, min_batch = 0, inflight = 0;
+  uint64_t window_ns = 0;
   uint8_t* h_in = nullptr;   // pinned ring: slot s at s * stride (plaintext, or ct || tag)
   uint8_t* z_in = nullptr;   // device alias
   uint8_t* h_out = nullptr;  // pinned ring: results (ct || tag, or plaintext)
   uint8_t* z_out = nullptr;
   std::unique_ptr<wgq::SlotMeta[]> meta;
-  wgq::IdQueue free_q, ready_q, done_q;
+  wgq::IdQueue done_q;                // completions: pushed by the dispatcher, popped by consumers
+  uint32_t lanes = 0, per_lane = 0;     // producer lanes and the ring slots each owns
+  std::unique_ptr<wgq::Lane[]> lane;
+  std::atomic<uint64_t> ready_hint{0};  // submissions not yet taken by the dispatcher (its sleep test)
   std::vector<wgq::Batch> batches;  // `inflight` launch buffers, used round robin
   DevBuf lpt_hist, lpt_order;       // the queue's own longest-first workspace (its own stream)
   hipStream_t stream = nullptr;
@@ -137,18 +169,19 @@ struct wg_queue {
 
 namespace {
 
-int queue_launch(wg_queue* q, wgq::Batch& b, uint32_t lmin, uint32_t lmax) {
+// One launch per batch: the kernel reads the batch's descriptors straight from pinned memory (no
+// copy), one packet per slot (WG_F_UNIFORM is only a scheduling hint: a queue batch is small, so no
+// longest-first ordering launches are worth their cost).
+int queue_launch(wg_queue* q, wgq::Batch& b, uint32_t lmax) {
   wg_ctx* c = q->c;
-  HIPTRY(hipMemcpyAsync(b.d_desc, b.h_desc, sizeof(wg_pkt) * b.n, hipMemcpyHostToDevice, q->stream));
-  const uint32_t flags = lmin == lmax ? WG_F_UNIFORM : 0u;
   const uint64_t size = (uint64_t)q->cap * q->stride;
   int rc;
   if (q->mode == WG_MODE_SEAL)
-    rc = launch_transport<WG_MODE_SEAL>(c, b.d_desc, b.n, q->z_in, size, q->z_out, size, nullptr, lmax, flags, q->stream,
-                                        nullptr, &q->lpt_hist, &q->lpt_order);
-  else
-    rc = launch_transport<WG_MODE_OPEN>(c, b.d_desc, b.n, q->z_in, size, q->z_out, size, b.z_status, lmax, flags,
+    rc = launch_transport<WG_MODE_SEAL>(c, b.z_desc, b.n, q->z_in, size, q->z_out, size, nullptr, lmax, WG_F_UNIFORM,
                                         q->stream, nullptr, &q->lpt_hist, &q->lpt_order);
+  else
+    rc = launch_transport<WG_MODE_OPEN>(c, b.z_desc, b.n, q->z_in, size, q->z_out, size, b.z_status, lmax,
+                                        WG_F_UNIFORM, q->stream, nullptr, &q->lpt_hist, &q->lpt_order);
   if (rc != WG_OK) return rc;
   HIPTRY(hipEventRecord(b.done, q->stream));
   return WG_OK;
@@ -173,8 +206,10 @@ void queue_complete(wg_queue* q, wgq::Batch& b, uint32_t status_override) {
 void queue_dispatch(wg_queue* q) {
   DeviceGuard g(q->c->device);
   uint32_t next = 0, oldest = 0, live = 0;  // batch ring: `live` in flight from `oldest`
+  uint32_t rr = 0;                          // lane the next gather starts at
   wgq::Batch* fill = &q->batches[next];
-  uint32_t lmin = ~0u, lmax = 0;
+  uint32_t lmax = 0;
+  uint64_t first_ns = 0;  // when the batch being filled took its first packet
   while (true) {
     // completions, oldest first
     while (live > 0) {
@@ -191,22 +226,32 @@ void queue_dispatch(wg_queue* q) {
     }
     // gather ready packets into the batch being filled
     if (live < q->inflight) {
-      uint32_t s;
-      while (fill->n < q->max_batch && q->ready_q.pop(&s)) {
-        const wgq::SlotMeta& m = q->meta[s];
-        wg_pkt& d = fill->h_desc[fill->n];
-        d.in_off = (uint64_t)s * q->stride;
-        d.out_off = (uint64_t)s * q->stride;
-        d.counter = m.counter;
-        d.len = m.len;
-        d.key_slot = m.key_slot;
-        fill->slots[fill->n++] = s;
-        lmin = std::min(lmin, m.len);
-        lmax = std::max(lmax, m.len);
+      uint32_t taken = 0;
+      for (uint32_t li = 0; li < q->lanes && fill->n < q->max_batch; ++li) {
+        wgq::Lane& ln = q->lane[(rr + li) % q->lanes];
+        const uint64_t t = ln.r_tail.load(std::memory_order_acquire);
+        uint64_t h = ln.r_head.load(std::memory_order_relaxed);
+        for (; h < t && fill->n < q->max_batch; ++h, ++taken) {
+          const uint32_t s = ln.ready[h % q->per_lane];
+          const wgq::SlotMeta& m = q->meta[s];
+          wg_pkt& d = fill->h_desc[fill->n];
+          d.in_off = (uint64_t)s * q->stride;
+          d.out_off = (uint64_t)s * q->stride;
+          d.counter = m.counter;
+          d.len = m.len;
+          d.key_slot = m.key_slot;
+          if (fill->n == 0) first_ns = wgq::now_ns();
+          fill->slots[fill->n++] = s;
+          lmax = std::max(lmax, m.len);
+        }
+        ln.r_head.store(h, std::memory_order_relaxed);
       }
-      // launch when the device is idle, or once min_batch packets wait while another batch runs
-      if (fill->n > 0 && (live == 0 || fill->n >= q->min_batch)) {
-        const int rc = queue_launch(q, *fill, lmin, lmax);
+      rr = (rr + 1) % q->lanes;
+      if (taken) q->ready_hint.fetch_sub(taken, std::memory_order_relaxed);
+      // launch once min_batch packets wait, or when the first of them has waited window_ns (a light
+      // load: one packet waits at most that long; a heavy one fills batches of min_batch and more)
+      if (fill->n > 0 && (fill->n >= q->min_batch || wgq::now_ns() - first_ns >= q->window_ns)) {
+        const int rc = queue_launch(q, *fill, lmax);
         if (rc != WG_OK) {
           q->err.store(rc);
           queue_complete(q, *fill, WG_PKT_FAILED);
@@ -215,20 +260,19 @@ void queue_dispatch(wg_queue* q) {
           next = (next + 1u) % q->inflight;
         }
         fill = &q->batches[next];
-        lmin = ~0u;
         lmax = 0;
         continue;
       }
     }
-    if (q->quit.load(std::memory_order_acquire) && live == 0) break;
-    if (live > 0) {
-      std::this_thread::yield();  // a batch runs: poll its event and the ready queue
+    if (q->quit.load(std::memory_order_acquire) && live == 0 && fill->n == 0) break;
+    if (live > 0 || fill->n > 0) {
+      std::this_thread::yield();  // a batch runs or one is filling: poll the events and the ready queue
       continue;
     }
     // nothing in flight and nothing ready: sleep until a producer pushes (or 1 ms)
     std::unique_lock<std::mutex> lk(q->mu);
     q->disp_idle.store(1, std::memory_order_seq_cst);
-    if (q->ready_q.size_hint() == 0 && !q->quit.load())
+    if (q->ready_hint.load() == 0 && !q->quit.load())
       q->cv_disp.wait_for(lk, std::chrono::milliseconds(1));
     q->disp_idle.store(0, std::memory_order_relaxed);
   }
@@ -237,7 +281,6 @@ void queue_dispatch(wg_queue* q) {
 void queue_free(wg_queue* q) {
   for (auto& b : q->batches) {
     if (b.h_desc) (void)hipHostFree(b.h_desc);
-    if (b.d_desc) (void)hipFree(b.d_desc);
     if (b.h_status) (void)hipHostFree(b.h_status);
     if (b.done) (void)hipEventDestroy(b.done);
   }
@@ -255,11 +298,19 @@ int queue_submit(wg_queue* q, int mode, uint32_t key_slot, uint64_t counter, con
   if (len > q->max_len) return fail(WG_E2BIG, "packet of %u bytes > the queue's max_len %u", len, q->max_len);
   if (key_slot >= q->c->key_slots) return fail(WG_ERANGE, "key slot %u", key_slot);
   if (const int e = q->err.load(std::memory_order_relaxed)) return fail(e, "queue failed earlier");
-  uint32_t s;
-  for (uint32_t spin = 0; !q->free_q.pop(&s); ++spin) {  // every slot in use: wait for a consumer
+  wgq::Lane& ln = q->lane[wgq::thread_number() % q->lanes];
+  wgq::spin_lock(ln.lock);
+  uint64_t fh = ln.f_head.load(std::memory_order_relaxed);
+  for (uint32_t spin = 0; fh == ln.f_tail.load(std::memory_order_acquire); ++spin) {
+    // every slot of this lane in use: wait for a consumer (without holding the lane)
+    wgq::spin_unlock(ln.lock);
     if (spin > 64u) std::this_thread::sleep_for(std::chrono::microseconds(10));
     else std::this_thread::yield();
+    wgq::spin_lock(ln.lock);
+    fh = ln.f_head.load(std::memory_order_relaxed);
   }
+  const uint32_t s = ln.freel[fh % q->per_lane];
+  ln.f_head.store(fh + 1, std::memory_order_relaxed);
   wgq::SlotMeta& m = q->meta[s];
   m.user = user;
   m.counter = counter;
@@ -268,7 +319,11 @@ int queue_submit(wg_queue* q, int mode, uint32_t key_slot, uint64_t counter, con
   m.t_submit_ns = wgq::now_ns();
   const size_t n = (size_t)len + (mode == WG_MODE_OPEN ? 16u : 0u);
   if (n) memcpy(q->h_in + (size_t)s * q->stride, src, n);
-  while (!q->ready_q.push(s)) std::this_thread::yield();  // holds at most cap ids: never full for long
+  const uint64_t rt = ln.r_tail.load(std::memory_order_relaxed);
+  ln.ready[rt % q->per_lane] = s;
+  ln.r_tail.store(rt + 1, std::memory_order_release);  // publish: after the slot's bytes and meta
+  wgq::spin_unlock(ln.lock);
+  q->ready_hint.fetch_add(1, std::memory_order_relaxed);
   if (q->disp_idle.load(std::memory_order_seq_cst)) {
     std::lock_guard<std::mutex> lk(q->mu);
     q->cv_disp.notify_one();
@@ -302,13 +357,27 @@ int wg_queue_create(wg_ctx* c, int mode, uint32_t capacity, uint32_t max_len, ui
   q->stride = ((max_len + 16u) + 63u) & ~63u;  // 64-B aligned slots: every payload read / store is 16-B aligned
   q->max_len = max_len;
   q->max_batch = std::min<uint32_t>(max_batch ? max_batch : 8192u, q->cap);
-  q->min_batch = std::max<uint32_t>(1u, std::min<uint32_t>(256u, q->max_batch / 4u));
-  q->inflight = 2;
+  // up to `inflight` batches run at once; while one runs, the next is launched once min_batch
+  // packets wait (WG_QUEUE_INFLIGHT / WG_QUEUE_MIN_BATCH override both for A/B runs)
+  q->inflight = 4;
+  q->min_batch = 512;
+  q->window_ns = 20000;
+  if (const char* e = getenv("WG_QUEUE_INFLIGHT")) q->inflight = std::max(1, std::min(16, atoi(e)));
+  if (const char* e = getenv("WG_QUEUE_MIN_BATCH")) q->min_batch = (uint32_t)std::max(1, atoi(e));
+  if (const char* e = getenv("WG_QUEUE_WINDOW_US")) q->window_ns = 1000ull * (uint64_t)std::max(0, atoi(e));
+  q->min_batch = std::min(q->min_batch, q->max_batch);
   q->meta.reset(new wgq::SlotMeta[q->cap]());
-  q->free_q.init(q->cap);
-  q->ready_q.init(q->cap);
   q->done_q.init(q->cap);
-  for (uint32_t s = 0; s < q->cap; ++s) q->free_q.push(s);
+  q->lanes = std::min<uint32_t>(64u, std::max<uint32_t>(1u, q->cap / 64u));
+  q->per_lane = q->cap / q->lanes;
+  q->lane.reset(new wgq::Lane[q->lanes]);
+  for (uint32_t l = 0; l < q->lanes; ++l) {
+    wgq::Lane& ln = q->lane[l];
+    ln.ready.reset(new uint32_t[q->per_lane]);
+    ln.freel.reset(new uint32_t[q->per_lane]);
+    for (uint32_t k = 0; k < q->per_lane; ++k) ln.freel[k] = l * q->per_lane + k;
+    ln.f_tail.store(q->per_lane);
+  }
   const size_t ring = (size_t)q->cap * q->stride;
   bool ok = hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking) == hipSuccess &&
             hipHostMalloc((void**)&q->h_in, ring, hipHostMallocMapped | hipHostMallocPortable) == hipSuccess &&
@@ -322,14 +391,15 @@ int wg_queue_create(wg_ctx* c, int mode, uint32_t capacity, uint32_t max_len, ui
   for (auto& b : q->batches) {
     if (!ok) break;
     b.slots.resize(q->max_batch);
-    ok = hipHostMalloc((void**)&b.h_desc, sizeof(wg_pkt) * q->max_batch, hipHostMallocPortable) == hipSuccess &&
-         hipMalloc((void**)&b.d_desc, sizeof(wg_pkt) * q->max_batch) == hipSuccess &&
+    ok = hipHostMalloc((void**)&b.h_desc, sizeof(wg_pkt) * q->max_batch, hipHostMallocMapped | hipHostMallocPortable) ==
+             hipSuccess &&
          hipHostMalloc((void**)&b.h_status, sizeof(uint32_t) * q->max_batch,
                        hipHostMallocMapped | hipHostMallocPortable) == hipSuccess &&
          hipEventCreateWithFlags(&b.done, hipEventDisableTiming) == hipSuccess;
     if (ok) {
       b.z_status = (uint32_t*)mapped_alias(b.h_status);
-      ok = b.z_status != nullptr;
+      b.z_desc = (wg_pkt*)mapped_alias(b.h_desc);
+      ok = b.z_status != nullptr && b.z_desc != nullptr;
     }
   }
   if (!ok) {
@@ -398,7 +468,13 @@ int wg_reap_done(wg_queue* q, const wg_completion* done, uint32_t n) {
   if (!q || (!done && n)) return fail(WG_EINVAL, "NULL argument");
   for (uint32_t i = 0; i < n; ++i) {
     if (done[i].slot >= q->cap) return fail(WG_EINVAL, "completion %u: slot %u", i, done[i].slot);
-    while (!q->free_q.push(done[i].slot)) std::this_thread::yield();
+    const uint32_t s = done[i].slot;
+    wgq::Lane& ln = q->lane[s / q->per_lane];
+    wgq::spin_lock(ln.flock);
+    const uint64_t ft = ln.f_tail.load(std::memory_order_relaxed);
+    ln.freel[ft % q->per_lane] = s;
+    ln.f_tail.store(ft + 1, std::memory_order_release);
+    wgq::spin_unlock(ln.flock);
   }
   return WG_OK;
 }
