@@ -7,6 +7,9 @@
 // a HIP kernel, and every entry point fails with WG_EDEVICE when no HIP device is usable.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <array>

@@ -337,7 +337,10 @@ __global__ void __launch_bounds__(64) k_pp(PPParams P) {
     if (quit) break;
     const uint64_t now = __builtin_amdgcn_s_memrealtime();
     const uint64_t l = ld_agent64(P.last);
-    const uint64_t since = now - (l > t0 ? l : t0);
+    // another wave may have stamped `last` after this wave read `now`: no idle time then (an unsigned
+    // now - l would wrap and end the server in the middle of its load)
+    const uint64_t ref = l > t0 ? l : t0;
+    const uint64_t since = now > ref ? now - ref : 0u;
     if (since > P.idle_ticks || now - t0 > P.life_ticks) {  // the whole server leaves together
       if (lane == 0) __hip_atomic_store(P.quit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
@@ -381,6 +384,16 @@ struct PPServer {
   uint32_t waves = 16, idle_us = 20000, life_ms = 250;
   std::atomic<uint64_t> launches{0}, packets{0};
   int fail_launches = 0;  // test hook (WG_PP_TEST_FAIL_LAUNCHES): refuse this many launches
+  uint32_t spin_limit = 4096;     // polls of the completion word before a waiting caller sleeps (WG_PP_SPIN)
+  uint32_t spin_callers = 12;     // more calls in flight than this: 64 polls, then sleep (WG_PP_SPIN_CALLERS)
+  std::atomic<uint32_t> active{0};  // calls between ticket and completion
+  // callers asleep on a futex per entry, woken by the waker thread (pp_sleep / pp_waker)
+  std::unique_ptr<std::atomic<uint32_t>[]> wake, waiting;
+  std::atomic<uint32_t> sleepers{0};
+  std::thread waker;
+  std::atomic<bool> waker_quit{false};
+  std::mutex wmu;
+  std::condition_variable wcv;
   uint64_t hold_counter = ~0ull;  // test hook (WG_PP_TEST_HOLD_COUNTER / _US): a call with this counter
   uint32_t hold_us = 0;           // sleeps between claiming its entry and publishing it
 
@@ -425,6 +438,14 @@ int pp_get(wg_ctx* c, PPServer** out) {
   if (const char* e = getenv("WG_PP_TEST_FAIL_LAUNCHES")) S->fail_launches = atoi(e);
   if (const char* e = getenv("WG_PP_TEST_HOLD_COUNTER")) S->hold_counter = strtoull(e, nullptr, 0);
   if (const char* e = getenv("WG_PP_TEST_HOLD_US")) S->hold_us = (uint32_t)atoi(e);
+  if (const char* e = getenv("WG_PP_SPIN")) S->spin_limit = (uint32_t)std::max(1, atoi(e));
+  if (const char* e = getenv("WG_PP_SPIN_CALLERS")) S->spin_callers = (uint32_t)std::max(0, atoi(e));
+  S->wake.reset(new std::atomic<uint32_t>[wgpp::kRing]);
+  S->waiting.reset(new std::atomic<uint32_t>[wgpp::kRing]);
+  for (uint32_t i = 0; i < wgpp::kRing; ++i) {
+    S->wake[i].store(0);
+    S->waiting[i].store(0);
+  }
   bool ok = hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking) == hipSuccess &&
             hipHostMalloc((void**)&S->host, S->bytes(), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
             hipHostGetDevicePointer((void**)&S->dev, S->host, 0) == hipSuccess &&
@@ -491,6 +512,12 @@ void pp_stop(wg_ctx* c) {
   }
   if (!S) return;
   DeviceGuard g(c->device);
+  {
+    std::lock_guard<std::mutex> lk(S->wmu);
+    S->waker_quit.store(true);
+    S->wcv.notify_all();
+  }
+  if (S->waker.joinable()) S->waker.join();
   S->ctl()->stop = 1;  // every wave sees it at its next poll and exits
   (void)hipStreamSynchronize(S->stream);
   pp_free(S);
@@ -546,6 +573,70 @@ int pp_big(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const uint
   return WG_OK;
 }
 
+long futex(std::atomic<uint32_t>* w, int op, uint32_t val, const struct timespec* t) {
+  return syscall(SYS_futex, (uint32_t*)w, op, val, t, nullptr, 0);
+}
+
+// The waker: while callers sleep (pp_sleep), one host thread polls their completion words and wakes
+// each caller whose result has landed (a futex per entry), and relaunches the server if it left.
+// Sleeping callers burn no CPU: 64 or 128 callers spinning on 16 cores exhaust a CPU quota early in
+// its period and are then all throttled until the next one (p999 ~70-90 ms).
+void pp_waker(PPServer* S) {
+  uint32_t iter = 0;
+  while (!S->waker_quit.load(std::memory_order_acquire)) {
+    if (S->sleepers.load(std::memory_order_acquire) == 0) {
+      std::unique_lock<std::mutex> lk(S->wmu);
+      S->wcv.wait_for(lk, std::chrono::milliseconds(10), [S] {
+        return S->sleepers.load() > 0 || S->waker_quit.load();
+      });
+      continue;
+    }
+    for (uint32_t i = 0; i < wgpp::kRing; ++i) {
+      if (!S->waiting[i].load(std::memory_order_acquire)) continue;
+      const uint64_t d = __atomic_load_n((const uint64_t*)S->done(i), __ATOMIC_ACQUIRE);
+      if ((d >> 8) == S->pub[i].load(std::memory_order_relaxed) && !S->wake[i].exchange(1))
+        futex(&S->wake[i], FUTEX_WAKE_PRIVATE, 1, nullptr);
+    }
+    if ((++iter & 63u) == 0) (void)pp_ensure(S);  // a server that left while callers sleep
+    for (int k = 0; k < 32; ++k) __builtin_ia32_pause();
+  }
+}
+
+// A caller whose completion has not landed within spin_limit polls sleeps on its entry's futex; the
+// waker (started with the first sleeper) wakes it. A 2-ms timeout re-checks the server on its own.
+int pp_sleep(PPServer* S, uint32_t i, uint64_t seq, uint64_t* d_out) {
+  {
+    std::lock_guard<std::mutex> lk(S->wmu);
+    if (!S->waker.joinable()) S->waker = std::thread(pp_waker, S);
+    S->waiting[i].store(1, std::memory_order_seq_cst);
+    S->sleepers.fetch_add(1, std::memory_order_seq_cst);
+    S->wcv.notify_one();
+  }
+  int rc = WG_OK;
+  const struct timespec to = {0, 2 * 1000 * 1000};
+  for (uint32_t naps = 0;; ++naps) {
+    S->wake[i].store(0, std::memory_order_seq_cst);
+    const uint64_t d = __atomic_load_n((const uint64_t*)S->done(i), __ATOMIC_ACQUIRE);
+    if ((d >> 8) == seq) {
+      *d_out = d;
+      break;
+    }
+    if ((naps & 255u) == 255u) {  // about half a second without a completion: is the device alive?
+      if ((rc = pp_ensure(S)) != WG_OK) break;
+      const hipError_t e = hipStreamQuery(S->stream);
+      if (e != hipSuccess && e != hipErrorNotReady) {
+        rc = fail(WG_EDEVICE, "per-packet server: %s", hipGetErrorString(e));
+        break;
+      }
+    }
+    futex(&S->wake[i], FUTEX_WAIT_PRIVATE, 0, &to);
+  }
+  S->waiting[i].store(0, std::memory_order_release);
+  S->sleepers.fetch_sub(1, std::memory_order_release);
+  return rc;
+}
+
+
 int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const uint8_t* src, uint32_t len,
               uint8_t* dst) {
   if (len > wgpp::kPPMaxLen) return pp_big(c, open, key_slot, counter, src, len, dst);
@@ -575,25 +666,22 @@ int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const u
   __atomic_fetch_xor(S->bell(i >> 6), 1ull << (i & 63u), __ATOMIC_SEQ_CST);
   rc = pp_ensure(S);
   uint64_t d = 0;
+  // with more calls in flight than spin_callers, a caller that polls for its whole round trip burns a
+  // core the host does not have (and under a CPU quota every thread of the process then stalls until
+  // the next quota period): it polls briefly and sleeps
+  const uint32_t in_flight = S->active.fetch_add(1, std::memory_order_relaxed) + 1u;
+  const uint32_t spin_limit = in_flight <= S->spin_callers ? S->spin_limit : 64u;
   for (uint64_t spin = 1; rc == WG_OK; ++spin) {
     d = __atomic_load_n((const uint64_t*)S->done(i), __ATOMIC_ACQUIRE);
     if ((d >> 8) == seq) break;
-    // long waits (more callers than cores): sleep instead of spinning, so the callers whose results
-    // have landed get a core (64 callers on 16 cores: spinning and yielding left p999 at 78 ms)
-    if (spin > 4096u) std::this_thread::sleep_for(std::chrono::microseconds(spin > 8192u ? 20 : 5));
-    if (spin == 100000u && getenv("WG_PP_DEBUG"))  // a call waiting for a second or more: say why
-      fprintf(stderr, "[wg_pp] entry %u seq %llu waits: done %llx bell %llx running %llu exit_flag %llu waves %u\n", i,
-              (unsigned long long)seq, (unsigned long long)d, (unsigned long long)*S->bell(i >> 6),
-              (unsigned long long)S->running.load(), (unsigned long long)*S->exit_flag(), S->waves);
-    if ((spin & 255u) == 0) {
-      rc = pp_ensure(S);  // the server may have left (idle / lifetime) before it saw this entry
-      if (rc == WG_OK && (spin & 0xfffffu) == 0) {
-        const hipError_t e = hipStreamQuery(S->stream);
-        if (e != hipSuccess && e != hipErrorNotReady) rc = fail(WG_EDEVICE, "per-packet server: %s", hipGetErrorString(e));
-      }
+    if (spin > spin_limit) {  // past the usual round trip: sleep until the waker sees the completion
+      rc = pp_sleep(S, i, seq, &d);
+      break;
     }
+    if ((spin & 255u) == 0) rc = pp_ensure(S);  // the server may have left (idle / lifetime) before it saw this entry
     __builtin_ia32_pause();
   }
+  S->active.fetch_sub(1, std::memory_order_relaxed);
   int result = rc;
   if (rc == WG_OK) {
     const uint32_t status = (uint32_t)(d & 0xffu);
