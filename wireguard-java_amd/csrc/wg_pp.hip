@@ -385,7 +385,7 @@ struct PPServer {
   std::atomic<uint64_t> launches{0}, packets{0};
   int fail_launches = 0;  // test hook (WG_PP_TEST_FAIL_LAUNCHES): refuse this many launches
   uint32_t spin_limit = 4096;     // polls of the completion word before a waiting caller sleeps (WG_PP_SPIN)
-  uint32_t spin_callers = 12;     // more calls in flight than this: 64 polls, then sleep (WG_PP_SPIN_CALLERS)
+  uint32_t spin_callers = ~0u;    // more calls in flight than this: 64 polls, then sleep (WG_PP_SPIN_CALLERS; off)
   std::atomic<uint32_t> active{0};  // calls between ticket and completion
   // callers asleep on a futex per entry, woken by the waker thread (pp_sleep / pp_waker)
   std::unique_ptr<std::atomic<uint32_t>[]> wake, waiting;
