@@ -332,7 +332,12 @@ def main():
     ap.add_argument("--workload", default="c1", choices=["c1", "c2", "c3", "c4"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-mem", default="pinned", choices=["pinned", "pageable"])
-    ap.add_argument("--streams", type=int, default=1)
+    # --streams K: each step's batch as K runs of consecutive packets, each sealed and opened on its own
+    # HIP stream (the same packets and bytes per step); 0 = auto: 2 for the uniform workloads, whose
+    # one-launch steps otherwise leave the machine partly idle while each launch's last waves drain
+    # (C1 +7-9% in an alternating A/B, profiles/r04_streams_ab.jsonl), 1 for C2 (its half batches
+    # take a different slot plan: -4%)
+    ap.add_argument("--streams", type=int, default=0)
     # duplex: each step is ONE wg_duplex_batch launch that seals this step's batch and opens
     # the previous step's ciphertext (double-buffered); serial: a seal launch, then an open
     # launch of the same batch
@@ -402,7 +407,7 @@ def main():
     # then opened on its own stream; the runs' kernels overlap, so one run's launch tail
     # is filled by another run's waves (the work and every packet's seal -> open order
     # are unchanged)
-    K = max(1, args.streams)
+    K = args.streams if args.streams > 0 else (2 if uniform and args.mode == "step" else 1)
     cuts = [n * i // K for i in range(K + 1)]
     main_stream = torch.cuda.current_stream()
     side = [main_stream] if K == 1 else [torch.cuda.Stream(device=dev) for _ in range(K)]
@@ -471,12 +476,19 @@ def main():
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     graph = None
     if args.graph:
-        if K != 1 or args.mode == "duplex":
-            raise SystemExit("--graph captures one stream of step launches (--streams 1, --mode step|serial)")
+        if args.mode == "duplex":
+            raise SystemExit("--graph captures step launches (--mode step|serial)")
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
+            cap = torch.cuda.current_stream()
+            if K > 1:  # the K streams' chains fork from and join back into the capture stream
+                for s_ in side:
+                    s_.wait_stream(cap)
             for _ in range(args.steps):
                 step()
+            if K > 1:
+                for s_ in side:
+                    cap.wait_stream(s_)
         graph.replay()  # warm: the graph's first launch
         torch.cuda.synchronize()
     if use_dist:
@@ -487,8 +499,10 @@ def main():
     if graph is not None:
         graph.replay()
     else:
+        fork()  # the K streams start after ev0 ...
         for _ in range(args.steps):
             step()
+        join()  # ... and ev1 waits for all of them
     t_enq = time.perf_counter()  # host time to enqueue the steps (the GPU idles if it is ~ ms_per_step)
     ev1.record()
     torch.cuda.synchronize()
@@ -497,6 +511,20 @@ def main():
         dist.barrier()
     elapsed = t1 - t0
     gpu_step_ms = ev0.elapsed_time(ev1) / args.steps  # = t_seal + t_open (back-to-back launches), or t_duplex
+
+    # K > 1: the launches of a step overlap, so a launch's duration is not its share of the step; the
+    # roofline of the dominant kernel comes from the same steps on ONE stream, timed right after (the
+    # kernel alone, back to back), and the value from the K-stream steps above
+    single_ms = None
+    if K > 1 and graph is None and args.mode == "step":
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(args.steps):
+            eng.duplex(d_desc, pt, ct, max_len, d_desc, ct, back, status, max_len, uniform=uniform, after_seal=True)
+        e1.record()
+        torch.cuda.synchronize()
+        single_ms = e0.elapsed_time(e1) / args.steps
 
     # per-kernel split (not in the timed region): seal-only and open-only launch trains
     def train(fn, k=10):
@@ -559,7 +587,7 @@ def main():
     D = importlib.import_module("wireguard-java_amd.dist")
     # transport kernel launches per step: k_duplex, or k_step (one WG_F_AFTER_SEAL step), or seal + open
     fused_step = args.mode == "step" and args.kernel in ("default", "transport") and args.variant == 0
-    launches = 1 if (args.mode == "duplex" or fused_step) else 2
+    launches = (1 if (args.mode == "duplex" or fused_step) else 2) * (K if args.mode != "duplex" else 1)
     # this rank's own figures, gathered before the max-over-ranks reduction (BASELINE configs[3]:
     # per-GPU and aggregate GiB/s)
     per_gpu = D.gather_per_rank(dist if use_dist else None, dev, {
@@ -575,7 +603,14 @@ def main():
     value = payload_all * args.steps / elapsed / GIB
     # seal reads L, writes L+16; open reads L+16, writes L -> 4L+32 per packet
     step_alg = float((4 * lengths + 32).sum())
-    achieved = step_alg / (gpu_step_ms * 1e-3) / 1e9
+    step_rate = step_alg / (gpu_step_ms * 1e-3) / 1e9  # the whole step (all K streams), GPU time
+    # the dominant kernel's roofline: one launch's algorithmic bytes over its duration (K = 1: the steps
+    # above; K > 1: the same steps on one stream, single_ms)
+    if single_ms is not None:
+        k_launches, k_ms = 1, single_ms
+    else:
+        k_launches, k_ms = launches, gpu_step_ms / launches
+    achieved = step_alg / k_launches / (k_ms * 1e-3) / 1e9
     pmc_mode = "fused" if fused_step else args.mode
     traffic = pmc_traffic(args.workload, pmc_mode)
     valu = pmc_valu_insts(args.workload, pmc_mode)
@@ -610,21 +645,27 @@ def main():
             "dtype": "u32",
             "data": "synthetic (random payload in HBM, splitmix64 keys, sequential counters)",
             "config": {"workload": wdesc, "packets_per_gpu": n, "payload_bytes": int(lengths.mean()), "step": args.mode,
+                       "streams": K,
                        "sessions_per_gpu": nkeys, "parallelism": f"dp{world} sharded by session, no collective"},
-            "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": kname + (", one stream" if single_ms is not None else ""),
+                         "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "alg_bytes_per_launch": int(step_alg / launches),
-                         "launches_per_step": launches, "kernel_names": knames,
-                         "kernel_ms": round(gpu_step_ms / launches, 5), "seal_ms": round(seal_ms, 5),
+                         "traffic": traffic, "alg_bytes_per_launch": int(step_alg / k_launches),
+                         "launches_per_step": k_launches, "kernel_names": knames,
+                         "kernel_ms": round(k_ms, 5), "seal_ms": round(seal_ms, 5),
                          "open_ms": round(open_ms, 5), "copy_gbs": round(copy_gbs, 1),
-                         "frac_of_copy": round(achieved / copy_gbs, 4)},
+                         "frac_of_copy": round(achieved / copy_gbs, 4),
+                         # the timed K-stream steps: their launches overlap (one stream's kernel tail is
+                         # filled by the next step on the other stream), so the rate per step is higher
+                         "step": {"streams": K, "launches": launches, "achieved": round(step_rate, 1),
+                                  "frac": round(step_rate / HBM_PEAK_GBS, 4), "ms": round(gpu_step_ms, 5)}},
             "verified": all_ok,
             "per_gpu": [{"rank": r["rank"], "gib_s": round(r["gib_s"], 2), "packets_per_step": r["packets"],
                          "elapsed_s": round(r["elapsed_s"], 6), "seal_ms": round(r["seal_ms"], 5),
                          "open_ms": round(r["open_ms"], 5), "kernel_ms": round(r["kernel_ms"], 5)} for r in per_gpu],
         }
         if valu:
-            rate = valu / (gpu_step_ms / launches * 1e-3)
+            rate = valu / (k_ms * 1e-3)
             line["valu_roofline"] = {"insts_per_launch": round(valu), "achieved": round(rate / 1e12, 4),
                                      "peak": round(VALU_PEAK_WIPS / 1e12, 4), "unit": "T wave-instr/s",
                                      "frac": round(rate / VALU_PEAK_WIPS, 4), "source": "SQ_INSTS_VALU, profiles/pmc_*.json"}
