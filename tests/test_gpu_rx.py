@@ -184,7 +184,30 @@ def test_reference_filter_known_answers_on_device(engine):
     assert got == [rx.PKT_OK, rx.PKT_FILTERED, rx.PKT_OK, rx.PKT_FILTERED]  # IPFilter.java:85-88
 
 
-def test_replay_window_batches_match_oracle(engine):
+@pytest.fixture(params=["fused", "five_launches"])
+def rp_engine(request, engine):
+    """The session engine (one k_rp_fused launch per check), or an engine whose replay checks take
+    the five-launch path (WG_RX_FUSED=0, read when the context's receive state is created)."""
+    import os
+    if request.param == "fused":
+        yield engine
+        return
+    old = os.environ.get("WG_RX_FUSED")
+    os.environ["WG_RX_FUSED"] = "0"
+    try:
+        e = wg().Engine(0, key_slots=4096)
+        e.replay_enable(64)
+    finally:
+        if old is None:
+            del os.environ["WG_RX_FUSED"]
+        else:
+            os.environ["WG_RX_FUSED"] = old
+    yield e
+    e.close()
+
+
+def test_replay_window_batches_match_oracle(rp_engine):
+    engine = rp_engine
     torch, dev = _dev()
     W = wg()
     Wb = 256
@@ -216,11 +239,12 @@ def test_replay_window_batches_match_oracle(engine):
     assert any(x == rx.PKT_REPLAY for x in want)
 
 
-def test_replay_sorted_batches_match_oracle(engine):
+def test_replay_sorted_batches_match_oracle(rp_engine):
     """Batches whose (slot, counter) pairs strictly increase with the index skip the duplicate
     table (k_rp_order); replays of earlier batches, old counters and window jumps must still be
     judged exactly as the oracle does. One batch repeats a pair (not strictly increasing) and
     so takes the table path."""
+    engine = rp_engine
     torch, dev = _dev()
     W = wg()
     Wb = 512
@@ -249,6 +273,45 @@ def test_replay_sorted_batches_match_oracle(engine):
         want = o.check_batch(slots, [int(x) for x in ctr], status)
         assert got == want, b
         for s_ in range(64):
+            top, words = engine.replay_state(s_, Wb)
+            otop, owords = o.bitmap(s_)
+            assert top == otop and [int(x) for x in words] == owords, (b, s_)
+    assert any(x == rx.PKT_REPLAY for x in want)
+
+
+@pytest.mark.parametrize("sorted_batch", [False, True])
+def test_replay_large_batches_span_grid_stride_loops(rp_engine, sorted_batch):
+    """Batches of 300,000 packets over 1024 key slots: k_rp_fused's grid (one block per CU) walks
+    each phase several times, reusing its per-block key lists; interleaved slots (the table path,
+    with duplicates) or the same packets sorted by (slot, counter) (no table)."""
+    engine = rp_engine
+    torch, dev = _dev()
+    W = wg()
+    Wb = 1024
+    engine.replay_enable(Wb)
+    engine.set_keys(0, splitmix_np(8, 32 * 1024).tobytes())
+    o = rx.ReplayWindow(Wb)
+    rng = np.random.default_rng(31 + sorted_batch)
+    base = np.zeros(1024, np.int64)
+    for b in range(3):
+        n = 300000
+        slots = rng.integers(0, 1024, n)
+        c64 = base[slots] + rng.integers(0, 700, n)
+        dup = rng.random(n) < 0.03
+        c64[dup] = np.maximum(c64[dup] - rng.integers(0, 1500, dup.sum()), 0)
+        if sorted_batch:
+            order = np.lexsort((c64, slots))
+            slots, c64 = slots[order], c64[order]
+            keep = np.ones(n, bool)
+            keep[1:] = (slots[1:] != slots[:-1]) | (c64[1:] != c64[:-1])
+            slots, c64 = slots[keep], c64[keep]
+        np.maximum.at(base, slots, c64)
+        ctr = c64.astype(np.uint64)
+        status = np.where(rng.random(len(slots)) < 0.01, 1, 0)
+        got = _run(engine, torch, dev, W, slots, ctr, [b""] * len(slots), status, W._lib.WG_RX_REPLAY)
+        want = o.check_batch(slots, [int(x) for x in ctr], status)
+        assert got == want, b
+        for s_ in range(0, 1024, 37):
             top, words = engine.replay_state(s_, Wb)
             otop, owords = o.bitmap(s_)
             assert top == otop and [int(x) for x in words] == owords, (b, s_)

@@ -4,7 +4,8 @@ with a 3-prefix AllowedIPs filter), after a 150-ms clock ramp:
   wg_rx_check alone: filter, replay, both; replay over 1024 key slots.
 HIP events on the launch stream around each of 200 calls (open variants: 200 calls each,
 alternating between the variants); the replay window is re-enabled (emptied, untimed) before each
-replay call so every call sees fresh counters."""
+replay call so every call sees fresh counters. WG_RX_FUSED=0 times the five-launch replay path
+(the default is one k_rp_fused launch)."""
 import json
 import os
 import sys
@@ -33,7 +34,7 @@ def main():
     dpt = torch.from_numpy(pt.reshape(-1)).to(dev)
     st0 = torch.zeros(n, dtype=torch.int32, device=dev)
     st = st0.clone()
-    out = {"n": n}
+    out = {"n": n, "rx_fused": os.environ.get("WG_RX_FUSED", "1") != "0"}
     eng.set_keys(0, bytes(range(32)))
     ct = torch.zeros_like(dpt)
     back = torch.zeros_like(dpt)

@@ -17,6 +17,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/resource.h>
 #include <time.h>
 
 #include "wgaead.h"
@@ -127,6 +128,27 @@ static void* verifier(void* arg) {
   return NULL;
 }
 
+/* the cgroup's CPU throttling counters (cgroup v2 cpu.stat), 0 where absent: the GPU box allows 16
+ * CPUs to a process that may run on all of them, and a run that exceeds the quota stalls every thread */
+static void throttled(unsigned long long* periods, unsigned long long* usec) {
+  *periods = *usec = 0;
+  FILE* f = fopen("/sys/fs/cgroup/cpu.stat", "r");
+  if (!f) return;
+  char k[64];
+  unsigned long long v;
+  while (fscanf(f, "%63s %llu", k, &v) == 2) {
+    if (!strcmp(k, "nr_throttled")) *periods = v;
+    if (!strcmp(k, "throttled_usec")) *usec = v;
+  }
+  fclose(f);
+}
+
+static double cpu_seconds(void) {
+  struct rusage r;
+  getrusage(RUSAGE_SELF, &r);
+  return r.ru_utime.tv_sec + r.ru_stime.tv_sec + 1e-6 * (r.ru_utime.tv_usec + r.ru_stime.tv_usec);
+}
+
 static int cmpd(const void* a, const void* b) {
   double x = *(const double*)a, y = *(const double*)b;
   return x < y ? -1 : x > y;
@@ -185,6 +207,9 @@ int main(int argc, char** argv) {
     return 2;
   }
   pthread_t th[256 + 16];
+  unsigned long long thp0, thu0, thp1, thu1;
+  throttled(&thp0, &thu0);
+  const double cpu0 = cpu_seconds();
   const uint64_t t0 = now_ns();
   for (int k = 0; k < nf; ++k) pthread_create(&th[g_P + k], NULL, forwarder, NULL);
   for (int k = 0; k < nv; ++k) pthread_create(&th[g_P + nf + k], NULL, verifier, NULL);
@@ -195,6 +220,8 @@ int main(int argc, char** argv) {
   const double t_sealed = (now_ns() - t0) * 1e-9;
   for (int k = 0; k < nv; ++k) pthread_join(th[g_P + nf + k], NULL);
   const double wall = (now_ns() - t0) * 1e-9;
+  const double cpu = cpu_seconds() - cpu0;
+  throttled(&thp1, &thu1);
   uint64_t bs = 0, ps = 0, bo = 0, po = 0;
   wg_queue_stats(g_qs, &bs, &ps);
   wg_queue_stats(g_qo, &bo, &po);
@@ -208,11 +235,13 @@ int main(int argc, char** argv) {
          "\"submit_gib_s\": %.3f, \"packets_per_s\": %.0f, "
          "\"seal_lat_us\": {\"p50\": %.1f, \"p99\": %.1f, \"p999\": %.1f, \"max\": %.1f}, "
          "\"open_lat_us\": {\"p50\": %.1f, \"p99\": %.1f, \"p999\": %.1f, \"max\": %.1f}, "
-         "\"seal_batches\": %llu, \"seal_mean_batch\": %.1f, \"open_batches\": %llu, \"open_mean_batch\": %.1f}\n",
+         "\"seal_batches\": %llu, \"seal_mean_batch\": %.1f, \"open_batches\": %llu, \"open_mean_batch\": %.1f, "
+         "\"cpu_s\": %.3f, \"cpus_busy\": %.2f, \"throttled_periods\": %llu, \"throttled_ms\": %.1f}\n",
          g_P, nf, nv, (unsigned long long)g_total, g_len ? argv[3] : "mixed 64..1500", max_batch,
          (unsigned long long)g_bad, wall, 2.0 * bytes / wall / gib, bytes / t_sealed / gib, bytes / t_submit / gib,
          g_total / wall, ls[0], ls[1], ls[2], ls[3], lo[0], lo[1], lo[2], lo[3], (unsigned long long)bs,
-         bs ? (double)ps / bs : 0.0, (unsigned long long)bo, bo ? (double)po / bo : 0.0);
+         bs ? (double)ps / bs : 0.0, (unsigned long long)bo, bo ? (double)po / bo : 0.0, cpu, cpu / wall,
+         thp1 - thp0, (thu1 - thu0) * 1e-3);
   wg_queue_destroy(g_qs);
   wg_queue_destroy(g_qo);
   wg_ctx_destroy(g_ctx);

@@ -7,8 +7,8 @@
 // wait for the crypto at all:
 //   producer (an FJP worker):  wg_submit_seal / wg_submit_open copy the packet into a free slot of a
 //       pinned, device-mapped ring and append the slot to its lane's ready ring (per-thread lanes,
-//       so producers share no cache line); they return at once (they block only when every slot of
-//       their lane is in use);
+//       so producers share no cache line; a lane with no free slot takes one from another lane);
+//       they return at once, and block (a futex) only when every slot of the ring is in use;
 //   dispatcher (one host thread per queue): pops ready slots into a batch, writes its descriptors
 //       into pinned memory and launches k_transport over the ring itself (zero-copy: the kernel
 //       reads descriptors and payload and writes the result over PCIe), at most `inflight` batches at a
@@ -86,7 +86,8 @@ struct IdQueue {
 };
 
 // Producers submit through lanes, so they never share a cache line with each other: a thread takes
-// lane (thread number mod lanes) of a queue, and a lane owns the ring slots [lane K, (lane + 1) K).
+// lane (thread number mod lanes) of a queue, and a lane owns the ring slots [lane K, (lane + 1) K)
+// (a slot taken by another lane's producer returns to its owner's free ring).
 // Its free list (slots the consumers handed back) and its ready list (slots filled and waiting for
 // the dispatcher) are single-producer / single-consumer rings; the lane lock is only contended when
 // two threads map to one lane, the free lock only among consumer threads.
@@ -155,6 +156,13 @@ struct wg_queue {
   uint32_t lanes = 0, per_lane = 0;     // producer lanes and the ring slots each owns
   std::unique_ptr<wgq::Lane[]> lane;
   std::atomic<uint64_t> ready_hint{0};  // submissions not yet taken by the dispatcher (its sleep test)
+  // producers that found no free slot sleep on `wake_word` until wg_reap_done has handed back
+  // wake_batch slots since the last wake (not one wake per freed slot: 16 producers woken for every
+  // reap burn the CPU the consumer needs to free slots, and fill the ring one packet at a time)
+  alignas(64) std::atomic<uint32_t> wake_word{0};
+  std::atomic<uint32_t> free_waiters{0};
+  alignas(64) std::atomic<uint32_t> freed_acc{0};
+  uint32_t wake_batch = 256;
   std::vector<wgq::Batch> batches;  // `inflight` launch buffers, used round robin
   DevBuf lpt_hist, lpt_order;       // the queue's own longest-first workspace (its own stream)
   hipStream_t stream = nullptr;
@@ -291,6 +299,47 @@ void queue_free(wg_queue* q) {
   if (q->stream) (void)hipStreamDestroy(q->stream);
 }
 
+// A free slot for a producer of lane `own` (its lock held): its own free ring first, then any other
+// lane's (try-lock only, so two producers taking from each other's lanes cannot deadlock). One
+// producer thread can so use the whole ring, not only its lane's share of it.
+bool queue_take_slot(wg_queue* q, wgq::Lane& own, uint32_t* s) {
+  uint64_t fh = own.f_head.load(std::memory_order_relaxed);
+  if (fh != own.f_tail.load(std::memory_order_acquire)) {
+    *s = own.freel[fh % q->per_lane];
+    own.f_head.store(fh + 1, std::memory_order_relaxed);
+    return true;
+  }
+  const uint32_t me = (uint32_t)(&own - q->lane.get());
+  for (uint32_t k = 1; k < q->lanes; ++k) {
+    wgq::Lane& o = q->lane[(me + k) % q->lanes];
+    fh = o.f_head.load(std::memory_order_relaxed);
+    if (fh == o.f_tail.load(std::memory_order_acquire)) continue;  // (a hint: checked again under the lock)
+    if (o.lock.exchange(1, std::memory_order_acquire)) continue;
+    fh = o.f_head.load(std::memory_order_relaxed);
+    const bool got = fh != o.f_tail.load(std::memory_order_acquire);
+    if (got) {
+      *s = o.freel[fh % q->per_lane];
+      o.f_head.store(fh + 1, std::memory_order_relaxed);
+    }
+    wgq::spin_unlock(o.lock);
+    if (got) return true;
+  }
+  return false;
+}
+
+// queue_take_slot with the lane lock taken.
+// Returns 1 (the lock stays held: the caller publishes), 0 (no free slot in any lane) or 2 (this
+// lane's ready ring is full: it holds at most per_lane slots, which slots taken from other lanes
+// could otherwise overflow; the dispatcher empties it within its next gather).
+int queue_try_slot(wg_queue* q, wgq::Lane& ln, uint32_t* s) {
+  wgq::spin_lock(ln.lock);
+  int r = 2;
+  if (ln.r_tail.load(std::memory_order_relaxed) - ln.r_head.load(std::memory_order_acquire) < q->per_lane)
+    r = queue_take_slot(q, ln, s) ? 1 : 0;
+  if (r != 1) wgq::spin_unlock(ln.lock);
+  return r;
+}
+
 int queue_submit(wg_queue* q, int mode, uint32_t key_slot, uint64_t counter, const uint8_t* src, uint32_t len,
                  uint64_t user) {
   if (!q || (!src && (len || mode == WG_MODE_OPEN))) return fail(WG_EINVAL, "NULL argument");
@@ -299,18 +348,27 @@ int queue_submit(wg_queue* q, int mode, uint32_t key_slot, uint64_t counter, con
   if (key_slot >= q->c->key_slots) return fail(WG_ERANGE, "key slot %u", key_slot);
   if (const int e = q->err.load(std::memory_order_relaxed)) return fail(e, "queue failed earlier");
   wgq::Lane& ln = q->lane[wgq::thread_number() % q->lanes];
-  wgq::spin_lock(ln.lock);
-  uint64_t fh = ln.f_head.load(std::memory_order_relaxed);
-  for (uint32_t spin = 0; fh == ln.f_tail.load(std::memory_order_acquire); ++spin) {
-    // every slot of this lane in use: wait for a consumer (without holding the lane)
-    wgq::spin_unlock(ln.lock);
-    if (spin > 64u) std::this_thread::sleep_for(std::chrono::microseconds(10));
-    else std::this_thread::yield();
-    wgq::spin_lock(ln.lock);
-    fh = ln.f_head.load(std::memory_order_relaxed);
+  uint32_t s = 0;
+  for (uint32_t round = 0;; ++round) {
+    const uint32_t w = q->wake_word.load(std::memory_order_acquire);
+    const int r = queue_try_slot(q, ln, &s);
+    if (r == 1) break;
+    // this lane's ready ring is full (the dispatcher is about to gather it), or every slot is in use:
+    // wait for wg_reap_done without burning the CPU the consumers need to free them
+    if (round < 2 || r == 2) {
+      if (round < 64) std::this_thread::yield();
+      else std::this_thread::sleep_for(std::chrono::microseconds(20));
+      continue;
+    }
+    q->free_waiters.fetch_add(1, std::memory_order_seq_cst);
+    if (queue_try_slot(q, ln, &s) == 1) {  // freed before this thread counted as a waiter
+      q->free_waiters.fetch_sub(1, std::memory_order_relaxed);
+      break;
+    }
+    const struct timespec ts = {0, 1000000};  // 1 ms: the last slots of a burst wake nobody
+    futex(&q->wake_word, FUTEX_WAIT_PRIVATE, w, &ts);
+    q->free_waiters.fetch_sub(1, std::memory_order_relaxed);
   }
-  const uint32_t s = ln.freel[fh % q->per_lane];
-  ln.f_head.store(fh + 1, std::memory_order_relaxed);
   wgq::SlotMeta& m = q->meta[s];
   m.user = user;
   m.counter = counter;
@@ -366,6 +424,7 @@ int wg_queue_create(wg_ctx* c, int mode, uint32_t capacity, uint32_t max_len, ui
   if (const char* e = getenv("WG_QUEUE_MIN_BATCH")) q->min_batch = (uint32_t)std::max(1, atoi(e));
   if (const char* e = getenv("WG_QUEUE_WINDOW_US")) q->window_ns = 1000ull * (uint64_t)std::max(0, atoi(e));
   q->min_batch = std::min(q->min_batch, q->max_batch);
+  q->wake_batch = std::max(1u, std::min(256u, q->cap / 8u));
   q->meta.reset(new wgq::SlotMeta[q->cap]());
   q->done_q.init(q->cap);
   q->lanes = std::min<uint32_t>(64u, std::max<uint32_t>(1u, q->cap / 64u));
@@ -475,6 +534,12 @@ int wg_reap_done(wg_queue* q, const wg_completion* done, uint32_t n) {
     ln.freel[ft % q->per_lane] = s;
     ln.f_tail.store(ft + 1, std::memory_order_release);
     wgq::spin_unlock(ln.flock);
+  }
+  if (n && q->freed_acc.fetch_add(n, std::memory_order_seq_cst) + n >= q->wake_batch &&
+      q->free_waiters.load(std::memory_order_seq_cst) > 0) {
+    q->freed_acc.store(0, std::memory_order_relaxed);
+    q->wake_word.fetch_add(1, std::memory_order_release);
+    futex(&q->wake_word, FUTEX_WAKE_PRIVATE, INT32_MAX, nullptr);
   }
   return WG_OK;
 }

@@ -59,6 +59,9 @@ struct RxState {
   uint32_t tab_size = 0;    // entries (a power of two >= 2n)
   DevBuf d_pos;             // per packet: its (slot, counter) entry in d_tab, or ~0
   DevBuf d_flag;            // k_rp_order's flag (0 between calls)
+  DevBuf d_bar;             // k_rp_fused's grid barrier {arrivals, generation} (arrivals 0 between calls)
+  bool fused = true;        // one k_rp_fused launch (WG_RX_FUSED=0: the five-launch path, for A/B)
+  uint32_t cus = 0;         // compute units: k_rp_fused's grid is at most one block per CU
   hipEvent_t ev = nullptr;  // last use of the replay scratch, and its stream (stream-ordered reuse)
   hipStream_t ev_stream = (hipStream_t)-1;
   DevBuf d_tables;          // wgt::RxTables for the fused open (WG_F_RX_FILTER)
@@ -107,7 +110,13 @@ uint32_t compile_level(const BinTrie& t, int32_t bnode, uint32_t depth, uint32_t
 }
 
 int rx_get(wg_ctx* c, RxState** out) {
-  if (!c->rx) c->rx = new RxState();
+  if (!c->rx) {
+    c->rx = new RxState();
+    if (const char* e = getenv("WG_RX_FUSED")) c->rx->fused = atoi(e) != 0;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && cus > 0)
+      c->rx->cus = (uint32_t)cus;
+  }
   *out = c->rx;
   return WG_OK;
 }
@@ -116,7 +125,7 @@ void rx_free(wg_ctx* c) {
   if (!c->rx) return;
   RxState* r = c->rx;
   for (DevBuf* b : {&r->d_entries, &r->d_hdr, &r->d_slot_filter, &r->d_top, &r->d_bits, &r->d_newtop, &r->d_tab,
-                    &r->d_pos, &r->d_flag, &r->d_tables})
+                    &r->d_pos, &r->d_flag, &r->d_bar, &r->d_tables})
     b->release();
   if (r->ev) (void)hipEventDestroy(r->ev);
   delete r;
@@ -305,6 +314,7 @@ __device__ __forceinline__ void block_group(bool active, uint64_t key, uint64_t 
       f(k, mx, orv);
     }
   }
+  __syncthreads();  // the list is reused by the block's next call (grid-stride loops of k_rp_fused)
 }
 
 // entry of (slot, counter) in the table of `size` (a power of two) entries (multiply-high)
@@ -315,8 +325,7 @@ __device__ __forceinline__ uint32_t rp_hash(uint32_t slot, uint64_t c, uint32_t 
 // A batch whose (key slot, counter) pairs strictly increase with the batch index (one peer's
 // in-order stream, or streams sorted by slot) holds no pair twice: the table is skipped. Only
 // a wave that finds an out-of-order neighbour raises the flag (no atomics in the common case).
-__global__ void __launch_bounds__(256) k_rp_order(RxParams P) {
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+__device__ __forceinline__ void rp_order_at(const RxParams& P, uint32_t i) {
   bool bad = false;
   if (i > 0 && i < P.n) {
     const wg_pkt a = P.desc[i - 1], b = P.desc[i];
@@ -327,12 +336,11 @@ __global__ void __launch_bounds__(256) k_rp_order(RxParams P) {
 
 // every candidate claims the entry of its (slot, counter): the first claim stores its batch index,
 // later claims of the same pair lower it to the smallest index (atomicMin); pos[i] = the entry
-__global__ void __launch_bounds__(256) k_rp_insert(RxParams P) {
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+__device__ __forceinline__ void rp_insert_at(const RxParams& P, uint32_t i, bool unsorted) {
   if (i >= P.n) return;
   uint32_t slot, pos = ~0u;
   uint64_t c;
-  if (*P.unsorted && rp_candidate(P, i, slot, c) && c < kRejectAfter) {
+  if (unsorted && rp_candidate(P, i, slot, c) && c < kRejectAfter) {
     const uint32_t mask = P.tab_size - 1u;
     uint32_t h = rp_hash(slot, c, P.tab_size);
     for (uint32_t probe = 0; probe < P.tab_size; ++probe, h = (h + 1u) & mask) {
@@ -358,14 +366,14 @@ __device__ __forceinline__ bool bit_test(const uint64_t* bits, uint32_t W, uint3
 }
 
 // a candidate passes if it is the lowest index of its (slot, counter) and the window as it stood
-// before the batch takes it; newtop[slot] = max(top, passing counter + 1)
-__global__ void __launch_bounds__(256) k_rp_decide(RxParams P) {
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+// before the batch takes it; newtop[slot] = max(top, passing counter + 1). Every thread of the
+// block calls it (block_group).
+__device__ __forceinline__ void rp_decide_at(const RxParams& P, uint32_t i, bool unsorted) {
   uint32_t slot = 0;
   uint64_t c = 0;
   const bool cand = i < P.n && rp_candidate(P, i, slot, c);
   bool ok = cand && c < kRejectAfter;
-  if (ok && *P.unsorted) ok = P.tab[P.pos[i]] == i;
+  if (ok && unsorted) ok = P.tab[P.pos[i]] == i;
   if (ok) {
     const uint64_t top = P.top[slot];
     if (c < top) ok = top - c <= P.window && !bit_test(P.bits, P.window, slot, c);
@@ -377,8 +385,7 @@ __global__ void __launch_bounds__(256) k_rp_decide(RxParams P) {
 }
 
 // per slot: the window moves to newtop; ring positions of the counters it passed are cleared
-__global__ void __launch_bounds__(256) k_rp_advance(RxParams P) {
-  const uint32_t slot = blockIdx.x * 256u + threadIdx.x;
+__device__ __forceinline__ void rp_advance_at(const RxParams& P, uint32_t slot) {
   if (slot >= P.key_slots) return;
   const uint64_t top = P.top[slot], nt = P.newtop[slot];
   if (nt <= top) return;
@@ -403,9 +410,9 @@ __global__ void __launch_bounds__(256) k_rp_advance(RxParams P) {
 }
 
 // accepted counters still inside the advanced window get their ring bit; the table entries this
-// batch used are emptied again (nothing reads the table in this kernel)
-__global__ void __launch_bounds__(256) k_rp_mark(RxParams P) {
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+// batch used are emptied again (nothing reads the table in this phase). Every thread of the block
+// calls it (block_group).
+__device__ __forceinline__ void rp_mark_at(const RxParams& P, uint32_t i, bool used_table) {
   uint32_t slot = 0;
   uint64_t c = 0;
   bool act = i < P.n && rp_candidate(P, i, slot, c);  // accepted packets are still OK
@@ -415,8 +422,64 @@ __global__ void __launch_bounds__(256) k_rp_mark(RxParams P) {
   block_group<false, true>(act, word, 1ull << (pos % 64), [&](uint64_t k, uint64_t, uint64_t orv) {
     atomicOr((unsigned long long*)&P.bits[k], (unsigned long long)orv);
   });
-  if (i < P.n && P.pos[i] != ~0u) P.tab[P.pos[i]] = ~0u;
+  if (used_table && i < P.n && P.pos[i] != ~0u) P.tab[P.pos[i]] = ~0u;
+}
+
+// The five phases as five launches (WG_RX_FUSED=0: the round-2 path, kept for A/B).
+__global__ void __launch_bounds__(256) k_rp_order(RxParams P) { rp_order_at(P, blockIdx.x * 256u + threadIdx.x); }
+__global__ void __launch_bounds__(256) k_rp_insert(RxParams P) {
+  rp_insert_at(P, blockIdx.x * 256u + threadIdx.x, *P.unsorted != 0);
+}
+__global__ void __launch_bounds__(256) k_rp_decide(RxParams P) {
+  rp_decide_at(P, blockIdx.x * 256u + threadIdx.x, *P.unsorted != 0);
+}
+__global__ void __launch_bounds__(256) k_rp_advance(RxParams P) { rp_advance_at(P, blockIdx.x * 256u + threadIdx.x); }
+__global__ void __launch_bounds__(256) k_rp_mark(RxParams P) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  rp_mark_at(P, i, true);  // k_rp_insert wrote every pos[i]
   if (i == 0) *P.unsorted = 0u;  // k_rp_decide was its last reader: 0 again for the next batch
+}
+
+// Grid barrier of k_rp_fused: every block must be resident (the grid is at most one block per CU,
+// and nothing this grid waits for needs a CU). `bar` = {arrivals, generation}; the last arrival
+// resets the count and opens the next generation, so the pair is ready for the next barrier and
+// the next launch. Agent-scope release before arriving, acquire after leaving: writes of every
+// block before the barrier are visible to every block after it (across the XCDs' L2s).
+__device__ __forceinline__ void rp_grid_barrier(uint32_t* bar) {
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t gen = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (atomicAdd(bar, 1u) == gridDim.x - 1u) {
+      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(bar + 1, gen + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      while (__hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen) __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  __threadfence();
+}
+
+// The whole window check in one launch: order flag | table inserts (unsorted batches only) |
+// decisions | window advance | marks, with a grid barrier between phases (3 barriers for a sorted
+// batch, 4 otherwise) instead of a kernel boundary. Grid-stride loops; every block runs every
+// iteration of each loop (block_group synchronises the block).
+__global__ void __launch_bounds__(256) k_rp_fused(RxParams P, uint32_t* bar) {
+  const uint32_t stride = gridDim.x * 256u;
+  for (uint32_t b = blockIdx.x * 256u; b < P.n; b += stride) rp_order_at(P, b + threadIdx.x);
+  rp_grid_barrier(bar);
+  const bool unsorted = __hip_atomic_load(P.unsorted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  if (unsorted) {  // uniform over the grid
+    for (uint32_t b = blockIdx.x * 256u; b < P.n; b += stride) rp_insert_at(P, b + threadIdx.x, true);
+    rp_grid_barrier(bar);
+  }
+  for (uint32_t b = blockIdx.x * 256u; b < P.n; b += stride) rp_decide_at(P, b + threadIdx.x, unsorted);
+  rp_grid_barrier(bar);
+  for (uint32_t b = blockIdx.x * 256u; b < P.key_slots; b += stride) rp_advance_at(P, b + threadIdx.x);
+  rp_grid_barrier(bar);
+  for (uint32_t b = blockIdx.x * 256u; b < P.n; b += stride) rp_mark_at(P, b + threadIdx.x, unsorted);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *P.unsorted = 0u;  // read by every block before the 2nd barrier
 }
 
 // keepalive / IP version / AllowedIPs, one thread per packet (wgt::rx_verdict, shared with the
@@ -597,8 +660,10 @@ int wg_rx_check(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* pt, ui
     if (T > r->tab_size) {  // (re)allocated, or reset after a failed check: all entries empty
       if ((rc = r->d_tab.ensure((size_t)T * 4)) != WG_OK) return rc;
       if ((rc = r->d_flag.ensure(4)) != WG_OK) return rc;
+      if ((rc = r->d_bar.ensure(8)) != WG_OK) return rc;
       HIPTRY(hipMemsetAsync(r->d_tab.p, 0xFF, (size_t)T * 4, s));
       HIPTRY(hipMemsetAsync(r->d_flag.p, 0, 4, s));
+      HIPTRY(hipMemsetAsync(r->d_bar.p, 0, 8, s));
       r->tab_size = T;
     }
     if ((rc = r->d_pos.ensure((size_t)n * 4)) != WG_OK) return rc;
@@ -610,11 +675,17 @@ int wg_rx_check(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* pt, ui
     P.tab_size = r->tab_size;
     P.pos = (uint32_t*)r->d_pos.p;
     P.unsorted = (uint32_t*)r->d_flag.p;
-    hipLaunchKernelGGL(wgrx::k_rp_order, dim3(grid), dim3(256), 0, s, P);
-    hipLaunchKernelGGL(wgrx::k_rp_insert, dim3(grid), dim3(256), 0, s, P);
-    hipLaunchKernelGGL(wgrx::k_rp_decide, dim3(grid), dim3(256), 0, s, P);
-    hipLaunchKernelGGL(wgrx::k_rp_advance, dim3((c->key_slots + 255u) / 256u), dim3(256), 0, s, P);
-    hipLaunchKernelGGL(wgrx::k_rp_mark, dim3(grid), dim3(256), 0, s, P);
+    if (r->fused && r->cus) {
+      // one launch, at most one block per CU (every block resident: the grid barriers need it)
+      const uint32_t fg = std::max(1u, std::min(r->cus, (std::max(n, c->key_slots) + 255u) / 256u));
+      hipLaunchKernelGGL(wgrx::k_rp_fused, dim3(fg), dim3(256), 0, s, P, (uint32_t*)r->d_bar.p);
+    } else {
+      hipLaunchKernelGGL(wgrx::k_rp_order, dim3(grid), dim3(256), 0, s, P);
+      hipLaunchKernelGGL(wgrx::k_rp_insert, dim3(grid), dim3(256), 0, s, P);
+      hipLaunchKernelGGL(wgrx::k_rp_decide, dim3(grid), dim3(256), 0, s, P);
+      hipLaunchKernelGGL(wgrx::k_rp_advance, dim3((c->key_slots + 255u) / 256u), dim3(256), 0, s, P);
+      hipLaunchKernelGGL(wgrx::k_rp_mark, dim3(grid), dim3(256), 0, s, P);
+    }
     const hipError_t le = hipGetLastError();
     if (le != hipSuccess) {
       r->tab_size = 0;  // the table / flag may be left dirty: the next check starts from empty ones
