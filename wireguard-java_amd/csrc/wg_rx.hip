@@ -449,7 +449,9 @@ __device__ __forceinline__ void rp_grid_barrier(uint32_t* bar) {
   __threadfence();
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t gen = __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // acquire: the arrival below is issued only after this read has returned (a generation read
+    // after the last arrival's increment would wait for the next one)
+    const uint32_t gen = __hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
     if (atomicAdd(bar, 1u) == gridDim.x - 1u) {
       __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(bar + 1, gen + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
