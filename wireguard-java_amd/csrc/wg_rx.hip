@@ -59,7 +59,7 @@ struct RxState {
   uint32_t tab_size = 0;    // entries (a power of two >= 2n)
   DevBuf d_pos;             // per packet: its (slot, counter) entry in d_tab, or ~0
   DevBuf d_flag;            // k_rp_order's flag (0 between calls)
-  DevBuf d_bar;             // k_rp_fused's grid barrier {arrivals, generation} (arrivals 0 between calls)
+  DevBuf d_bar;             // k_rp_fused's grid barrier {arrivals, generation, overrun flag} (arrivals 0 between calls)
   bool fused = true;        // one k_rp_fused launch (WG_RX_FUSED=0: the five-launch path, for A/B)
   uint32_t cus = 0;         // compute units: k_rp_fused's grid is at most one block per CU
   hipEvent_t ev = nullptr;  // last use of the replay scratch, and its stream (stream-ordered reuse)
@@ -456,7 +456,15 @@ __device__ __forceinline__ void rp_grid_barrier(uint32_t* bar) {
       __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(bar + 1, gen + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      while (__hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen) __builtin_amdgcn_s_sleep(1);
+      // bounded (about a second): a grid that cannot be co-resident must not hang the device; the
+      // overrun is recorded in bar[2] (wg_replay_state reports it)
+      for (uint32_t spin = 0; __hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen; ++spin) {
+        if (spin > (1u << 24)) {
+          atomicOr(bar + 2, 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
     }
   }
   __syncthreads();
@@ -622,7 +630,10 @@ int wg_replay_state(wg_ctx* c, uint32_t slot, uint64_t* top, uint64_t* bits, uin
   if (bits)
     HIPTRY(hipMemcpyAsync(bits, (uint64_t*)r->d_bits.p + (size_t)slot * words, (size_t)words * 8,
                           hipMemcpyDeviceToHost, c->stream));
+  uint32_t overrun = 0;
+  if (r->d_bar.p) HIPTRY(hipMemcpyAsync(&overrun, (uint32_t*)r->d_bar.p + 2, 4, hipMemcpyDeviceToHost, c->stream));
   HIPTRY(hipStreamSynchronize(c->stream));
+  if (overrun) return fail(WG_EDEVICE, "a replay check's grid barrier timed out: its window state is not valid");
   return WG_OK;
 }
 
@@ -662,10 +673,10 @@ int wg_rx_check(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* pt, ui
     if (T > r->tab_size) {  // (re)allocated, or reset after a failed check: all entries empty
       if ((rc = r->d_tab.ensure((size_t)T * 4)) != WG_OK) return rc;
       if ((rc = r->d_flag.ensure(4)) != WG_OK) return rc;
-      if ((rc = r->d_bar.ensure(8)) != WG_OK) return rc;
+      if ((rc = r->d_bar.ensure(16)) != WG_OK) return rc;
       HIPTRY(hipMemsetAsync(r->d_tab.p, 0xFF, (size_t)T * 4, s));
       HIPTRY(hipMemsetAsync(r->d_flag.p, 0, 4, s));
-      HIPTRY(hipMemsetAsync(r->d_bar.p, 0, 8, s));
+      HIPTRY(hipMemsetAsync(r->d_bar.p, 0, 16, s));
       r->tab_size = T;
     }
     if ((rc = r->d_pos.ensure((size_t)n * 4)) != WG_OK) return rc;
