@@ -184,24 +184,24 @@ def test_reference_filter_known_answers_on_device(engine):
     assert got == [rx.PKT_OK, rx.PKT_FILTERED, rx.PKT_OK, rx.PKT_FILTERED]  # IPFilter.java:85-88
 
 
-@pytest.fixture(params=["fused", "five_launches"])
+@pytest.fixture(params=["four_launches", "five_launches"])
 def rp_engine(request, engine):
-    """The session engine (one k_rp_fused launch per check), or an engine whose replay checks take
-    the five-launch path (WG_RX_FUSED=0, read when the context's receive state is created)."""
+    """The session engine (decide and advance in one launch), or an engine whose replay checks
+    launch them separately (WG_RX_LAUNCHES=5, read when the context's receive state is created)."""
     import os
-    if request.param == "fused":
+    if request.param == "four_launches":
         yield engine
         return
-    old = os.environ.get("WG_RX_FUSED")
-    os.environ["WG_RX_FUSED"] = "0"
+    old = os.environ.get("WG_RX_LAUNCHES")
+    os.environ["WG_RX_LAUNCHES"] = "5"
     try:
         e = wg().Engine(0, key_slots=4096)
         e.replay_enable(64)
     finally:
         if old is None:
-            del os.environ["WG_RX_FUSED"]
+            del os.environ["WG_RX_LAUNCHES"]
         else:
-            os.environ["WG_RX_FUSED"] = old
+            os.environ["WG_RX_LAUNCHES"] = old
     yield e
     e.close()
 
@@ -281,8 +281,8 @@ def test_replay_sorted_batches_match_oracle(rp_engine):
 
 @pytest.mark.parametrize("sorted_batch", [False, True])
 def test_replay_large_batches_span_grid_stride_loops(rp_engine, sorted_batch):
-    """Batches of 300,000 packets over 1024 key slots: k_rp_fused's grid (one block per CU) walks
-    each phase several times, reusing its per-block key lists; interleaved slots (the table path,
+    """Batches of 300,000 packets over 1024 key slots (1,172 blocks racing to be the last of
+    k_rp_decide_adv, every slot's new top spread over 8 copies): interleaved slots (the table path,
     with duplicates) or the same packets sorted by (slot, counter) (no table)."""
     engine = rp_engine
     torch, dev = _dev()

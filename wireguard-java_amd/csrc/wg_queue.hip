@@ -98,6 +98,11 @@ struct Lane {
   alignas(64) std::atomic<uint32_t> flock{0};   // free ring pushes (consumers)
   std::atomic<uint64_t> f_tail{0};
   alignas(64) std::atomic<uint64_t> f_head{0};  // free ring pops: under `lock`
+  // slots this lane's producer took from other lanes (under `lock`): taken kStash at a time, so a
+  // producer whose own slots are all in flight scans the other lanes once per kStash packets
+  static constexpr uint32_t kStash = 32;
+  uint32_t nstash = 0, hint = 0;
+  uint32_t stash[kStash];
   std::unique_ptr<uint32_t[]> ready, freel;     // K entries each
 };
 
@@ -163,6 +168,7 @@ struct wg_queue {
   std::atomic<uint32_t> free_waiters{0};
   alignas(64) std::atomic<uint32_t> freed_acc{0};
   uint32_t wake_batch = 256;
+  bool steal = true;  // a producer whose lane has no free slot takes one from another lane (WG_QUEUE_STEAL=0: no)
   std::vector<wgq::Batch> batches;  // `inflight` launch buffers, used round robin
   DevBuf lpt_hist, lpt_order;       // the queue's own longest-first workspace (its own stream)
   hipStream_t stream = nullptr;
@@ -309,20 +315,34 @@ bool queue_take_slot(wg_queue* q, wgq::Lane& own, uint32_t* s) {
     own.f_head.store(fh + 1, std::memory_order_relaxed);
     return true;
   }
+  if (own.nstash) {
+    *s = own.stash[--own.nstash];
+    return true;
+  }
+  if (!q->steal) return false;
   const uint32_t me = (uint32_t)(&own - q->lane.get());
-  for (uint32_t k = 1; k < q->lanes; ++k) {
-    wgq::Lane& o = q->lane[(me + k) % q->lanes];
+  for (uint32_t k = 0; k < q->lanes; ++k) {
+    const uint32_t v = (own.hint + k) % q->lanes;
+    if (v == me) continue;
+    wgq::Lane& o = q->lane[v];
     fh = o.f_head.load(std::memory_order_relaxed);
     if (fh == o.f_tail.load(std::memory_order_acquire)) continue;  // (a hint: checked again under the lock)
     if (o.lock.exchange(1, std::memory_order_acquire)) continue;
     fh = o.f_head.load(std::memory_order_relaxed);
-    const bool got = fh != o.f_tail.load(std::memory_order_acquire);
-    if (got) {
-      *s = o.freel[fh % q->per_lane];
-      o.f_head.store(fh + 1, std::memory_order_relaxed);
+    const uint64_t avail = o.f_tail.load(std::memory_order_acquire) - fh;
+    // half of what the victim has free (its own producer keeps the rest), at most a stash
+    const uint32_t take = (uint32_t)std::min<uint64_t>(wgq::Lane::kStash + 1u, (avail + 1u) / 2u);
+    for (uint32_t t = 0; t < take; ++t) {
+      const uint32_t x = o.freel[(fh + t) % q->per_lane];
+      if (t == 0) *s = x;
+      else own.stash[own.nstash++] = x;
     }
+    o.f_head.store(fh + take, std::memory_order_relaxed);
     wgq::spin_unlock(o.lock);
-    if (got) return true;
+    if (take) {
+      own.hint = v;
+      return true;
+    }
   }
   return false;
 }
@@ -423,6 +443,7 @@ int wg_queue_create(wg_ctx* c, int mode, uint32_t capacity, uint32_t max_len, ui
   if (const char* e = getenv("WG_QUEUE_INFLIGHT")) q->inflight = std::max(1, std::min(16, atoi(e)));
   if (const char* e = getenv("WG_QUEUE_MIN_BATCH")) q->min_batch = (uint32_t)std::max(1, atoi(e));
   if (const char* e = getenv("WG_QUEUE_WINDOW_US")) q->window_ns = 1000ull * (uint64_t)std::max(0, atoi(e));
+  if (const char* e = getenv("WG_QUEUE_STEAL")) q->steal = atoi(e) != 0;
   q->min_batch = std::min(q->min_batch, q->max_batch);
   q->wake_batch = std::max(1u, std::min(256u, q->cap / 8u));
   q->meta.reset(new wgq::SlotMeta[q->cap]());
@@ -525,15 +546,36 @@ int wg_reap(wg_queue* q, wg_completion* out, uint32_t max, uint32_t timeout_us) 
 
 int wg_reap_done(wg_queue* q, const wg_completion* done, uint32_t n) {
   if (!q || (!done && n)) return fail(WG_EINVAL, "NULL argument");
-  for (uint32_t i = 0; i < n; ++i) {
+  for (uint32_t i = 0; i < n; ++i)
     if (done[i].slot >= q->cap) return fail(WG_EINVAL, "completion %u: slot %u", i, done[i].slot);
-    const uint32_t s = done[i].slot;
-    wgq::Lane& ln = q->lane[s / q->per_lane];
-    wgq::spin_lock(ln.flock);
-    const uint64_t ft = ln.f_tail.load(std::memory_order_relaxed);
-    ln.freel[ft % q->per_lane] = s;
-    ln.f_tail.store(ft + 1, std::memory_order_release);
-    wgq::spin_unlock(ln.flock);
+  // grouped by home lane: one lock and one tail store per lane and chunk, not per slot (the free
+  // ring's tail shares a cache line with the lane's producer, which reads it for every packet)
+  constexpr uint32_t kChunk = 512;
+  uint32_t cnt[64], at[64], tmp[kChunk];
+  for (uint32_t c0 = 0; c0 < n; c0 += kChunk) {
+    const uint32_t m = std::min(kChunk, n - c0);
+    for (uint32_t l = 0; l < q->lanes; ++l) cnt[l] = 0;
+    for (uint32_t i = 0; i < m; ++i) ++cnt[done[c0 + i].slot / q->per_lane];
+    uint32_t acc = 0;
+    for (uint32_t l = 0; l < q->lanes; ++l) {
+      at[l] = acc;
+      acc += cnt[l];
+    }
+    for (uint32_t i = 0; i < m; ++i) {
+      const uint32_t sl = done[c0 + i].slot;
+      tmp[at[sl / q->per_lane]++] = sl;
+    }
+    uint32_t k = 0;
+    for (uint32_t l = 0; l < q->lanes; ++l) {
+      if (!cnt[l]) continue;
+      wgq::Lane& ln = q->lane[l];
+      wgq::spin_lock(ln.flock);
+      const uint64_t ft = ln.f_tail.load(std::memory_order_relaxed);
+      for (uint32_t j = 0; j < cnt[l]; ++j) ln.freel[(ft + j) % q->per_lane] = tmp[k + j];
+      ln.f_tail.store(ft + cnt[l], std::memory_order_release);
+      wgq::spin_unlock(ln.flock);
+      k += cnt[l];
+    }
   }
   if (n && q->freed_acc.fetch_add(n, std::memory_order_seq_cst) + n >= q->wake_batch &&
       q->free_waiters.load(std::memory_order_seq_cst) > 0) {

@@ -34,9 +34,11 @@
 // ever accepted twice. oracle/rx.py restates these rules one packet at a time.
 // Kernels: k_rp_order flags a batch whose (slot, counter) pairs do not strictly increase with
 // the index (only then can a pair repeat); k_rp_insert claims one entry per (slot, counter) pair in an open-addressing table
-// (lowest index by atomicMin), k_rp_decide judges against the old window, k_rp_advance moves
-// each slot's window, k_rp_mark sets the ring bits and empties the table again. Atomics on a
-// shared address (a slot's new top, a window word) are aggregated per workgroup first.
+// (lowest index by atomicMin), k_rp_decide_adv judges against the old window and its last block
+// moves each slot's window (k_rp_decide + k_rp_advance for tables of more than 4096 slots),
+// k_rp_mark sets the ring bits and empties the table again. Atomics on a shared address (a
+// slot's new top, a window word) are aggregated per workgroup first; new tops are spread over 8
+// copies per slot.
 #pragma once
 
 namespace {
@@ -44,6 +46,8 @@ namespace {
 constexpr uint32_t kRxNoFilter = 0xFFFFFFFFu;
 constexpr uint64_t kRejectAfter = ~0ull - 8191ull - 1ull;  // 2^64 - 2^13 - 1
 constexpr uint64_t kEmptyKey = ~0ull;                      // counters that large are rejected first
+constexpr uint32_t kTopWays = 8;         // copies of each slot's new top (spread same-address atomics)
+constexpr uint32_t kAdvanceInline = 4096;  // key slots the last block of k_rp_decide_adv advances
 
 struct RxState {
   // AllowedIPs: host copies of each filter's compiled tables; device image rebuilt on change
@@ -54,14 +58,12 @@ struct RxState {
   // replay window
   uint32_t window = 0;      // W bits (0: disabled)
   DevBuf d_top, d_bits;     // per slot: u64 top; W/64 u64 words
-  DevBuf d_newtop;          // per slot: the window's new top while a batch is checked (== top between calls)
+  DevBuf d_newtop;          // per slot, kTopWays copies: the window's new top while a batch is checked (== top between calls)
   DevBuf d_tab;             // (slot, counter) -> lowest batch index, open addressing; all empty between calls
   uint32_t tab_size = 0;    // entries (a power of two >= 2n)
   DevBuf d_pos;             // per packet: its (slot, counter) entry in d_tab, or ~0
-  DevBuf d_flag;            // k_rp_order's flag (0 between calls)
-  DevBuf d_bar;             // k_rp_fused's grid barrier {arrivals, generation, overrun flag} (arrivals 0 between calls)
-  bool fused = true;        // one k_rp_fused launch (WG_RX_FUSED=0: the five-launch path, for A/B)
-  uint32_t cus = 0;         // compute units: k_rp_fused's grid is at most one block per CU
+  DevBuf d_flag;            // {k_rp_order's flag, k_rp_decide_adv's finished blocks} (0 between calls)
+  bool five = false;        // WG_RX_LAUNCHES=5: decide and advance as two launches (A/B)
   hipEvent_t ev = nullptr;  // last use of the replay scratch, and its stream (stream-ordered reuse)
   hipStream_t ev_stream = (hipStream_t)-1;
   DevBuf d_tables;          // wgt::RxTables for the fused open (WG_F_RX_FILTER)
@@ -112,10 +114,7 @@ uint32_t compile_level(const BinTrie& t, int32_t bnode, uint32_t depth, uint32_t
 int rx_get(wg_ctx* c, RxState** out) {
   if (!c->rx) {
     c->rx = new RxState();
-    if (const char* e = getenv("WG_RX_FUSED")) c->rx->fused = atoi(e) != 0;
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && cus > 0)
-      c->rx->cus = (uint32_t)cus;
+    if (const char* e = getenv("WG_RX_LAUNCHES")) c->rx->five = atoi(e) == 5;
   }
   *out = c->rx;
   return WG_OK;
@@ -125,7 +124,7 @@ void rx_free(wg_ctx* c) {
   if (!c->rx) return;
   RxState* r = c->rx;
   for (DevBuf* b : {&r->d_entries, &r->d_hdr, &r->d_slot_filter, &r->d_top, &r->d_bits, &r->d_newtop, &r->d_tab,
-                    &r->d_pos, &r->d_flag, &r->d_bar, &r->d_tables})
+                    &r->d_pos, &r->d_flag, &r->d_tables})
     b->release();
   if (r->ev) (void)hipEventDestroy(r->ev);
   delete r;
@@ -169,7 +168,7 @@ int rx_reset_slots(wg_ctx* c, uint32_t first, uint32_t n, hipStream_t s) {
   int rc;
   if ((rc = rx_after_last_check(r, s)) != WG_OK) return rc;
   HIPTRY(hipMemsetAsync((uint64_t*)r->d_top.p + first, 0, (size_t)n * 8, s));
-  HIPTRY(hipMemsetAsync((uint64_t*)r->d_newtop.p + first, 0, (size_t)n * 8, s));
+  HIPTRY(hipMemsetAsync((uint64_t*)r->d_newtop.p + (size_t)first * kTopWays, 0, (size_t)n * 8 * kTopWays, s));
   const size_t words = r->window / 64;
   HIPTRY(hipMemsetAsync((uint64_t*)r->d_bits.p + (size_t)first * words, 0, (size_t)n * words * 8, s));
   if (!r->ev) HIPTRY(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming));
@@ -204,6 +203,7 @@ struct RxParams {
   uint32_t tab_size;
   uint32_t* pos;
   uint32_t* unsorted;  // 0 while the batch's (slot, counter) pairs strictly increase with the index
+  uint32_t* done_blocks;  // k_rp_decide_adv: blocks finished (0 between calls)
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -314,7 +314,6 @@ __device__ __forceinline__ void block_group(bool active, uint64_t key, uint64_t 
       f(k, mx, orv);
     }
   }
-  __syncthreads();  // the list is reused by the block's next call (grid-stride loops of k_rp_fused)
 }
 
 // entry of (slot, counter) in the table of `size` (a power of two) entries (multiply-high)
@@ -378,16 +377,27 @@ __device__ __forceinline__ void rp_decide_at(const RxParams& P, uint32_t i, bool
     const uint64_t top = P.top[slot];
     if (c < top) ok = top - c <= P.window && !bit_test(P.bits, P.window, slot, c);
   }
+  // newtop has kTopWays copies per slot (block b raises copy b mod kTopWays): a batch of one slot
+  // raises one address from every block, and same-address atomics serialise at memory
+  const uint32_t way = blockIdx.x % kTopWays;
   block_group<true, false>(ok, slot, c + 1, [&](uint64_t k, uint64_t mx, uint64_t) {
-    atomicMax((unsigned long long*)&P.newtop[k], (unsigned long long)mx);
+    atomicMax((unsigned long long*)&P.newtop[k * kTopWays + way], (unsigned long long)mx);
   });
   if (cand && !ok) P.status[i] = WG_PKT_REPLAY;
 }
 
-// per slot: the window moves to newtop; ring positions of the counters it passed are cleared
+// per slot: the window moves to newtop (the largest of its kTopWays copies, read as device-scope
+// atomics: in k_rp_decide_adv the last block reads what every block raised); ring positions of the
+// counters it passed are cleared and every copy is set to the new top again
 __device__ __forceinline__ void rp_advance_at(const RxParams& P, uint32_t slot) {
   if (slot >= P.key_slots) return;
-  const uint64_t top = P.top[slot], nt = P.newtop[slot];
+  const uint64_t top = P.top[slot];
+  uint64_t nt = top;
+#pragma unroll
+  for (uint32_t w = 0; w < kTopWays; ++w) {
+    const uint64_t v = __hip_atomic_load(&P.newtop[slot * kTopWays + w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    nt = v > nt ? v : nt;
+  }
   if (nt <= top) return;
   const uint32_t W = P.window, words = W / 64;
   uint64_t* b = P.bits + (uint64_t)slot * words;
@@ -407,12 +417,14 @@ __device__ __forceinline__ void rp_advance_at(const RxParams& P, uint32_t slot) 
     }
   }
   P.top[slot] = nt;
+#pragma unroll
+  for (uint32_t w = 0; w < kTopWays; ++w) P.newtop[slot * kTopWays + w] = nt;
 }
 
 // accepted counters still inside the advanced window get their ring bit; the table entries this
 // batch used are emptied again (nothing reads the table in this phase). Every thread of the block
 // calls it (block_group).
-__device__ __forceinline__ void rp_mark_at(const RxParams& P, uint32_t i, bool used_table) {
+__device__ __forceinline__ void rp_mark_at(const RxParams& P, uint32_t i) {
   uint32_t slot = 0;
   uint64_t c = 0;
   bool act = i < P.n && rp_candidate(P, i, slot, c);  // accepted packets are still OK
@@ -422,10 +434,13 @@ __device__ __forceinline__ void rp_mark_at(const RxParams& P, uint32_t i, bool u
   block_group<false, true>(act, word, 1ull << (pos % 64), [&](uint64_t k, uint64_t, uint64_t orv) {
     atomicOr((unsigned long long*)&P.bits[k], (unsigned long long)orv);
   });
-  if (used_table && i < P.n && P.pos[i] != ~0u) P.tab[P.pos[i]] = ~0u;
+  if (i < P.n && P.pos[i] != ~0u) P.tab[P.pos[i]] = ~0u;
 }
 
-// The five phases as five launches (WG_RX_FUSED=0: the round-2 path, kept for A/B).
+// The phases as launches: order | insert | decide (+ advance) | mark. For tables of at most
+// kAdvanceInline key slots the last block of k_rp_decide_adv to finish advances every slot's window
+// (no launch of its own); larger tables take k_rp_decide + k_rp_advance (WG_RX_LAUNCHES=5 forces
+// that path for A/B).
 __global__ void __launch_bounds__(256) k_rp_order(RxParams P) { rp_order_at(P, blockIdx.x * 256u + threadIdx.x); }
 __global__ void __launch_bounds__(256) k_rp_insert(RxParams P) {
   rp_insert_at(P, blockIdx.x * 256u + threadIdx.x, *P.unsorted != 0);
@@ -434,62 +449,23 @@ __global__ void __launch_bounds__(256) k_rp_decide(RxParams P) {
   rp_decide_at(P, blockIdx.x * 256u + threadIdx.x, *P.unsorted != 0);
 }
 __global__ void __launch_bounds__(256) k_rp_advance(RxParams P) { rp_advance_at(P, blockIdx.x * 256u + threadIdx.x); }
+__global__ void __launch_bounds__(256) k_rp_decide_adv(RxParams P) {
+  rp_decide_at(P, blockIdx.x * 256u + threadIdx.x, *P.unsorted != 0);
+  // every atomicMax of this block has completed before the block counts itself done, so the last
+  // block's device-scope loads see every block's new tops (no cache flush needed)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ uint32_t last;
+  if (threadIdx.x == 0) last = atomicAdd(P.done_blocks, 1u) == gridDim.x - 1u;
+  __syncthreads();
+  if (!last) return;
+  for (uint32_t slot = threadIdx.x; slot < P.key_slots; slot += 256u) rp_advance_at(P, slot);
+  if (threadIdx.x == 0) *P.done_blocks = 0u;  // for the next check (the kernel boundary orders it)
+}
 __global__ void __launch_bounds__(256) k_rp_mark(RxParams P) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  rp_mark_at(P, i, true);  // k_rp_insert wrote every pos[i]
+  rp_mark_at(P, i);
   if (i == 0) *P.unsorted = 0u;  // k_rp_decide was its last reader: 0 again for the next batch
-}
-
-// Grid barrier of k_rp_fused: every block must be resident (the grid is at most one block per CU,
-// and nothing this grid waits for needs a CU). `bar` = {arrivals, generation}; the last arrival
-// resets the count and opens the next generation, so the pair is ready for the next barrier and
-// the next launch. Agent-scope release before arriving, acquire after leaving: writes of every
-// block before the barrier are visible to every block after it (across the XCDs' L2s).
-__device__ __forceinline__ void rp_grid_barrier(uint32_t* bar) {
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    // acquire: the arrival below is issued only after this read has returned (a generation read
-    // after the last arrival's increment would wait for the next one)
-    const uint32_t gen = __hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    if (atomicAdd(bar, 1u) == gridDim.x - 1u) {
-      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(bar + 1, gen + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      // bounded (about a second): a grid that cannot be co-resident must not hang the device; the
-      // overrun is recorded in bar[2] (wg_replay_state reports it)
-      for (uint32_t spin = 0; __hip_atomic_load(bar + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen; ++spin) {
-        if (spin > (1u << 24)) {
-          atomicOr(bar + 2, 1u);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-  }
-  __syncthreads();
-  __threadfence();
-}
-
-// The whole window check in one launch: order flag | table inserts (unsorted batches only) |
-// decisions | window advance | marks, with a grid barrier between phases (3 barriers for a sorted
-// batch, 4 otherwise) instead of a kernel boundary. Grid-stride loops; every block runs every
-// iteration of each loop (block_group synchronises the block).
-__global__ void __launch_bounds__(256) k_rp_fused(RxParams P, uint32_t* bar) {
-  const uint32_t stride = gridDim.x * 256u;
-  for (uint32_t b = blockIdx.x * 256u; b < P.n; b += stride) rp_order_at(P, b + threadIdx.x);
-  rp_grid_barrier(bar);
-  const bool unsorted = __hip_atomic_load(P.unsorted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-  if (unsorted) {  // uniform over the grid
-    for (uint32_t b = blockIdx.x * 256u; b < P.n; b += stride) rp_insert_at(P, b + threadIdx.x, true);
-    rp_grid_barrier(bar);
-  }
-  for (uint32_t b = blockIdx.x * 256u; b < P.n; b += stride) rp_decide_at(P, b + threadIdx.x, unsorted);
-  rp_grid_barrier(bar);
-  for (uint32_t b = blockIdx.x * 256u; b < P.key_slots; b += stride) rp_advance_at(P, b + threadIdx.x);
-  rp_grid_barrier(bar);
-  for (uint32_t b = blockIdx.x * 256u; b < P.n; b += stride) rp_mark_at(P, b + threadIdx.x, unsorted);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *P.unsorted = 0u;  // read by every block before the 2nd barrier
 }
 
 // keepalive / IP version / AllowedIPs, one thread per packet (wgt::rx_verdict, shared with the
@@ -597,7 +573,7 @@ int wg_replay_enable(wg_ctx* c, uint32_t window_bits) {
   if (!window_bits) return WG_OK;
   int rc;
   if ((rc = r->d_top.ensure((size_t)c->key_slots * 8)) != WG_OK ||
-      (rc = r->d_newtop.ensure((size_t)c->key_slots * 8)) != WG_OK ||
+      (rc = r->d_newtop.ensure((size_t)c->key_slots * 8 * kTopWays)) != WG_OK ||
       (rc = r->d_bits.ensure((size_t)c->key_slots * (window_bits / 8))) != WG_OK)
     return rc;
   if ((rc = rx_reset_slots(c, 0, c->key_slots, c->stream)) != WG_OK) return rc;
@@ -630,10 +606,7 @@ int wg_replay_state(wg_ctx* c, uint32_t slot, uint64_t* top, uint64_t* bits, uin
   if (bits)
     HIPTRY(hipMemcpyAsync(bits, (uint64_t*)r->d_bits.p + (size_t)slot * words, (size_t)words * 8,
                           hipMemcpyDeviceToHost, c->stream));
-  uint32_t overrun = 0;
-  if (r->d_bar.p) HIPTRY(hipMemcpyAsync(&overrun, (uint32_t*)r->d_bar.p + 2, 4, hipMemcpyDeviceToHost, c->stream));
   HIPTRY(hipStreamSynchronize(c->stream));
-  if (overrun) return fail(WG_EDEVICE, "a replay check's grid barrier timed out: its window state is not valid");
   return WG_OK;
 }
 
@@ -672,11 +645,9 @@ int wg_rx_check(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* pt, ui
       HIPTRY(hipDeviceSynchronize());  // the scratch is reallocated under earlier checks
     if (T > r->tab_size) {  // (re)allocated, or reset after a failed check: all entries empty
       if ((rc = r->d_tab.ensure((size_t)T * 4)) != WG_OK) return rc;
-      if ((rc = r->d_flag.ensure(4)) != WG_OK) return rc;
-      if ((rc = r->d_bar.ensure(16)) != WG_OK) return rc;
+      if ((rc = r->d_flag.ensure(8)) != WG_OK) return rc;
       HIPTRY(hipMemsetAsync(r->d_tab.p, 0xFF, (size_t)T * 4, s));
-      HIPTRY(hipMemsetAsync(r->d_flag.p, 0, 4, s));
-      HIPTRY(hipMemsetAsync(r->d_bar.p, 0, 16, s));
+      HIPTRY(hipMemsetAsync(r->d_flag.p, 0, 8, s));
       r->tab_size = T;
     }
     if ((rc = r->d_pos.ensure((size_t)n * 4)) != WG_OK) return rc;
@@ -688,17 +659,16 @@ int wg_rx_check(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* pt, ui
     P.tab_size = r->tab_size;
     P.pos = (uint32_t*)r->d_pos.p;
     P.unsorted = (uint32_t*)r->d_flag.p;
-    if (r->fused && r->cus) {
-      // one launch, at most one block per CU (every block resident: the grid barriers need it)
-      const uint32_t fg = std::max(1u, std::min(r->cus, (std::max(n, c->key_slots) + 255u) / 256u));
-      hipLaunchKernelGGL(wgrx::k_rp_fused, dim3(fg), dim3(256), 0, s, P, (uint32_t*)r->d_bar.p);
+    P.done_blocks = (uint32_t*)r->d_flag.p + 1;
+    hipLaunchKernelGGL(wgrx::k_rp_order, dim3(grid), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(wgrx::k_rp_insert, dim3(grid), dim3(256), 0, s, P);
+    if (!r->five && c->key_slots <= kAdvanceInline) {
+      hipLaunchKernelGGL(wgrx::k_rp_decide_adv, dim3(grid), dim3(256), 0, s, P);
     } else {
-      hipLaunchKernelGGL(wgrx::k_rp_order, dim3(grid), dim3(256), 0, s, P);
-      hipLaunchKernelGGL(wgrx::k_rp_insert, dim3(grid), dim3(256), 0, s, P);
       hipLaunchKernelGGL(wgrx::k_rp_decide, dim3(grid), dim3(256), 0, s, P);
       hipLaunchKernelGGL(wgrx::k_rp_advance, dim3((c->key_slots + 255u) / 256u), dim3(256), 0, s, P);
-      hipLaunchKernelGGL(wgrx::k_rp_mark, dim3(grid), dim3(256), 0, s, P);
     }
+    hipLaunchKernelGGL(wgrx::k_rp_mark, dim3(grid), dim3(256), 0, s, P);
     const hipError_t le = hipGetLastError();
     if (le != hipSuccess) {
       r->tab_size = 0;  // the table / flag may be left dirty: the next check starts from empty ones
