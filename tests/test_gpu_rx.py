@@ -186,16 +186,16 @@ def test_reference_filter_known_answers_on_device(engine):
 
 @pytest.fixture(params=["four_launches", "five_launches"])
 def rp_engine(request, engine):
-    """The session engine (decide and advance in one launch), or an engine whose replay checks
-    launch them separately (WG_RX_LAUNCHES=5, read when the context's receive state is created)."""
+    """An engine whose replay checks run in four launches (order, insert, decide + advance, mark) or
+    with decide and advance launched separately (WG_RX_LAUNCHES=5, read when the context's receive
+    state is created)."""
     import os
-    if request.param == "four_launches":
-        yield engine
-        return
     old = os.environ.get("WG_RX_LAUNCHES")
-    os.environ["WG_RX_LAUNCHES"] = "5"
+    os.environ["WG_RX_LAUNCHES"] = "4" if request.param == "four_launches" else "5"
     try:
-        e = wg().Engine(0, key_slots=4096)
+        # at most 512 key slots: the last block of k_rp_decide_adv advances them (larger tables launch
+        # k_rp_advance whatever WG_RX_LAUNCHES says)
+        e = wg().Engine(0, key_slots=512)
         e.replay_enable(64)
     finally:
         if old is None:
@@ -280,8 +280,8 @@ def test_replay_sorted_batches_match_oracle(rp_engine):
 
 
 @pytest.mark.parametrize("sorted_batch", [False, True])
-def test_replay_large_batches_span_grid_stride_loops(rp_engine, sorted_batch):
-    """Batches of 300,000 packets over 1024 key slots (1,172 blocks racing to be the last of
+def test_replay_large_batches_many_slots(rp_engine, sorted_batch):
+    """Batches of 300,000 packets over 512 key slots (1,172 blocks racing to be the last of
     k_rp_decide_adv, every slot's new top spread over 8 copies): interleaved slots (the table path,
     with duplicates) or the same packets sorted by (slot, counter) (no table)."""
     engine = rp_engine
@@ -289,13 +289,13 @@ def test_replay_large_batches_span_grid_stride_loops(rp_engine, sorted_batch):
     W = wg()
     Wb = 1024
     engine.replay_enable(Wb)
-    engine.set_keys(0, splitmix_np(8, 32 * 1024).tobytes())
+    engine.set_keys(0, splitmix_np(8, 32 * 512).tobytes())
     o = rx.ReplayWindow(Wb)
     rng = np.random.default_rng(31 + sorted_batch)
-    base = np.zeros(1024, np.int64)
+    base = np.zeros(512, np.int64)
     for b in range(3):
         n = 300000
-        slots = rng.integers(0, 1024, n)
+        slots = rng.integers(0, 512, n)
         c64 = base[slots] + rng.integers(0, 700, n)
         dup = rng.random(n) < 0.03
         c64[dup] = np.maximum(c64[dup] - rng.integers(0, 1500, dup.sum()), 0)
@@ -311,7 +311,7 @@ def test_replay_large_batches_span_grid_stride_loops(rp_engine, sorted_batch):
         got = _run(engine, torch, dev, W, slots, ctr, [b""] * len(slots), status, W._lib.WG_RX_REPLAY)
         want = o.check_batch(slots, [int(x) for x in ctr], status)
         assert got == want, b
-        for s_ in range(0, 1024, 37):
+        for s_ in range(0, 512, 17):
             top, words = engine.replay_state(s_, Wb)
             otop, owords = o.bitmap(s_)
             assert top == otop and [int(x) for x in words] == owords, (b, s_)

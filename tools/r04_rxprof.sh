@@ -17,11 +17,11 @@ for r in rows:
     dur[r['Kernel_Name'].split('(')[0]].append(int(r['End_Timestamp']) - int(r['Start_Timestamp']))
 for k, v in dur.items():
     v.sort(); print(k, len(v), 'median ns', v[len(v)//2])
-# calls: a k_rp_order or k_rp_fused starts a call; span = first start .. last end of the call
+# calls: a k_rp_order starts a call; span = first start .. last end of the call
 calls, cur = [], []
 for r in rows:
     n = r['Kernel_Name']
-    if ('k_rp_order' in n or 'k_rp_decide_adv' in n and False) and cur:
+    if ('k_rp_order' in n) and cur:
         calls.append(cur); cur = []
     cur.append(r)
 if cur: calls.append(cur)

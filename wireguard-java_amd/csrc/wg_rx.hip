@@ -35,7 +35,7 @@
 // Kernels: k_rp_order flags a batch whose (slot, counter) pairs do not strictly increase with
 // the index (only then can a pair repeat); k_rp_insert claims one entry per (slot, counter) pair in an open-addressing table
 // (lowest index by atomicMin), k_rp_decide_adv judges against the old window and its last block
-// moves each slot's window (k_rp_decide + k_rp_advance for tables of more than 4096 slots),
+// moves each slot's window (k_rp_decide + k_rp_advance for tables of more than 512 slots),
 // k_rp_mark sets the ring bits and empties the table again. Atomics on a shared address (a
 // slot's new top, a window word) are aggregated per workgroup first; new tops are spread over 8
 // copies per slot.
@@ -47,7 +47,10 @@ constexpr uint32_t kRxNoFilter = 0xFFFFFFFFu;
 constexpr uint64_t kRejectAfter = ~0ull - 8191ull - 1ull;  // 2^64 - 2^13 - 1
 constexpr uint64_t kEmptyKey = ~0ull;                      // counters that large are rejected first
 constexpr uint32_t kTopWays = 8;         // copies of each slot's new top (spread same-address atomics)
-constexpr uint32_t kAdvanceInline = 4096;  // key slots the last block of k_rp_decide_adv advances
+// key slots the last block of k_rp_decide_adv advances: one peer's 64K packets in order 25 us per
+// check against 31 as separate launches, but 1024 interleaved slots 65 against 60 (the last block
+// walks every slot), so larger tables launch the advance (profiles/r04_rx_launches.txt)
+constexpr uint32_t kAdvanceInline = 512;
 
 struct RxState {
   // AllowedIPs: host copies of each filter's compiled tables; device image rebuilt on change
@@ -389,16 +392,7 @@ __device__ __forceinline__ void rp_decide_at(const RxParams& P, uint32_t i, bool
 // per slot: the window moves to newtop (the largest of its kTopWays copies, read as device-scope
 // atomics: in k_rp_decide_adv the last block reads what every block raised); ring positions of the
 // counters it passed are cleared and every copy is set to the new top again
-__device__ __forceinline__ void rp_advance_at(const RxParams& P, uint32_t slot) {
-  if (slot >= P.key_slots) return;
-  const uint64_t top = P.top[slot];
-  uint64_t nt = top;
-#pragma unroll
-  for (uint32_t w = 0; w < kTopWays; ++w) {
-    const uint64_t v = __hip_atomic_load(&P.newtop[slot * kTopWays + w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    nt = v > nt ? v : nt;
-  }
-  if (nt <= top) return;
+__device__ __forceinline__ void rp_advance_to(const RxParams& P, uint32_t slot, uint64_t top, uint64_t nt) {
   const uint32_t W = P.window, words = W / 64;
   uint64_t* b = P.bits + (uint64_t)slot * words;
   if (nt - top >= W) {
@@ -420,6 +414,17 @@ __device__ __forceinline__ void rp_advance_at(const RxParams& P, uint32_t slot) 
 #pragma unroll
   for (uint32_t w = 0; w < kTopWays; ++w) P.newtop[slot * kTopWays + w] = nt;
 }
+__device__ __forceinline__ void rp_advance_at(const RxParams& P, uint32_t slot) {
+  if (slot >= P.key_slots) return;
+  const uint64_t top = P.top[slot];
+  uint64_t nt = top;
+#pragma unroll
+  for (uint32_t w = 0; w < kTopWays; ++w) {
+    const uint64_t v = __hip_atomic_load(&P.newtop[slot * kTopWays + w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    nt = v > nt ? v : nt;
+  }
+  if (nt > top) rp_advance_to(P, slot, top, nt);
+}
 
 // accepted counters still inside the advanced window get their ring bit; the table entries this
 // batch used are emptied again (nothing reads the table in this phase). Every thread of the block
@@ -437,10 +442,11 @@ __device__ __forceinline__ void rp_mark_at(const RxParams& P, uint32_t i) {
   if (i < P.n && P.pos[i] != ~0u) P.tab[P.pos[i]] = ~0u;
 }
 
-// The phases as launches: order | insert | decide (+ advance) | mark. For tables of at most
-// kAdvanceInline key slots the last block of k_rp_decide_adv to finish advances every slot's window
-// (no launch of its own); larger tables take k_rp_decide + k_rp_advance (WG_RX_LAUNCHES=5 forces
-// that path for A/B).
+// The phases as launches: k_rp_order | k_rp_insert (skipped for a strictly increasing batch) |
+// k_rp_decide_adv (its last block to finish advances every slot's window) | k_rp_mark. Tables of
+// more than kAdvanceInline key slots (and WG_RX_LAUNCHES=5, for A/B) take k_rp_decide +
+// k_rp_advance instead of k_rp_decide_adv. (Inserting every pair to drop the order check made the
+// insert 21 us instead of 3: the table's CAS-with-return round trips cost more than a launch.)
 __global__ void __launch_bounds__(256) k_rp_order(RxParams P) { rp_order_at(P, blockIdx.x * 256u + threadIdx.x); }
 __global__ void __launch_bounds__(256) k_rp_insert(RxParams P) {
   rp_insert_at(P, blockIdx.x * 256u + threadIdx.x, *P.unsorted != 0);
@@ -455,11 +461,57 @@ __global__ void __launch_bounds__(256) k_rp_decide_adv(RxParams P) {
   // block's device-scope loads see every block's new tops (no cache flush needed)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  __shared__ uint32_t last;
-  if (threadIdx.x == 0) last = atomicAdd(P.done_blocks, 1u) == gridDim.x - 1u;
+  __shared__ uint32_t last, nfull, full[64];
+  if (threadIdx.x == 0) {
+    last = atomicAdd(P.done_blocks, 1u) == gridDim.x - 1u;
+    nfull = 0;
+  }
   __syncthreads();
   if (!last) return;
-  for (uint32_t slot = threadIdx.x; slot < P.key_slots; slot += 256u) rp_advance_at(P, slot);
+  // a slot whose window moves by W or more has every word cleared: by the whole block (a batch of
+  // one peer's 64K packets clears 128 words), listed here; every other advance runs per thread
+  const uint32_t words = P.window / 64;
+  constexpr uint32_t U = 4;  // slots per thread whose loads are in flight together (one latency, not U)
+  for (uint32_t base = 0; base < P.key_slots; base += 256u * U) {
+    uint64_t tops[U], nts[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t slot = base + threadIdx.x + 256u * u;
+      tops[u] = nts[u] = 0;
+      if (slot < P.key_slots) {
+        tops[u] = nts[u] = P.top[slot];
+#pragma unroll
+        for (uint32_t w = 0; w < kTopWays; ++w) {
+          const uint64_t v =
+              __hip_atomic_load(&P.newtop[slot * kTopWays + w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          nts[u] = v > nts[u] ? v : nts[u];
+        }
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+    const uint32_t slot = base + threadIdx.x + 256u * u;
+    const uint64_t top = tops[u], nt = nts[u];
+    if (slot >= P.key_slots || nt <= top) continue;
+    if (nt - top >= P.window && words > 8u) {
+      const uint32_t e = atomicAdd(&nfull, 1u);
+      if (e < 64u) {
+        full[e] = slot;
+        P.top[slot] = nt;
+#pragma unroll
+        for (uint32_t w = 0; w < kTopWays; ++w) P.newtop[slot * kTopWays + w] = nt;
+        continue;
+      }
+    }
+    rp_advance_to(P, slot, top, nt);
+    }
+  }
+  __syncthreads();
+  const uint32_t nf = min(nfull, 64u);
+  for (uint32_t f = 0; f < nf; ++f) {
+    uint64_t* b = P.bits + (uint64_t)full[f] * words;
+    for (uint32_t k = threadIdx.x; k < words; k += 256u) b[k] = 0;
+  }
   if (threadIdx.x == 0) *P.done_blocks = 0u;  // for the next check (the kernel boundary orders it)
 }
 __global__ void __launch_bounds__(256) k_rp_mark(RxParams P) {
