@@ -118,6 +118,12 @@ int wg_sync(wg_ctx* ctx, void* stream); /* hipStreamSynchronize */
 const char* wg_last_error(void);        /* thread-local text for the last error */
 const char* wg_version(void);
 
+/* NUMA node of HIP device `device`'s PCI function (sysfs), or -1 if unknown. A queue's dispatcher
+ * thread runs on that node's CPUs (wg_queue_create); callers feeding the GPU from many threads
+ * should place them there too (TransportManager's pools: numactl --cpunodebind, or a thread
+ * factory that sets the affinity). */
+int wg_device_numa_node(int device);
+
 /* Transport kernel used by this context's wg_seal_batch / wg_open_batch / *_host calls
  * (a test and A/B hook beside the reference interface). name: "default"
  * or NULL or "transport" (k_transport, the product kernel), "wave1" (the round-1

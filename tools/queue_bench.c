@@ -11,7 +11,9 @@
  * Output: one JSON line: seal+open payload GiB/s over the whole run (both directions' payload bytes,
  * as bench.py's cpu_baseline counts them), seal-side rate, latency percentiles per queue (submit ->
  * reap), batches per queue. Exit status 1 on any failed status or byte mismatch. */
+#define _GNU_SOURCE
 #include <pthread.h>
+#include <sched.h>
 #include <stdatomic.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -149,6 +151,30 @@ static double cpu_seconds(void) {
   return r.ru_utime.tv_sec + r.ru_stime.tv_sec + 1e-6 * (r.ru_utime.tv_usec + r.ru_stime.tv_usec);
 }
 
+/* the CPUs of NUMA node `node` from sysfs ("0-63,128-191"); 0 if unreadable */
+static int node_cpus(int node, cpu_set_t* set) {
+  char path[96], buf[4096];
+  if (node < 0) return 0;
+  snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+  FILE* f = fopen(path, "r");
+  if (!f) return 0;
+  const int ok = fgets(buf, sizeof buf, f) != NULL;
+  fclose(f);
+  if (!ok) return 0;
+  CPU_ZERO(set);
+  int n = 0;
+  for (char* p = buf; *p && *p != '\n';) {
+    char* e;
+    const long a = strtol(p, &e, 10);
+    if (e == p) break;
+    long b = a;
+    if (*e == '-') b = strtol(e + 1, &e, 10);
+    for (long c = a; c <= b && c < CPU_SETSIZE; ++c, ++n) CPU_SET((int)c, set);
+    p = *e == ',' ? e + 1 : e;
+  }
+  return n;
+}
+
 static int cmpd(const void* a, const void* b) {
   double x = *(const double*)a, y = *(const double*)b;
   return x < y ? -1 : x > y;
@@ -175,6 +201,19 @@ int main(int argc, char** argv) {
   if (g_P < 1 || g_P > 256 || g_N < 1 || g_len < 0 || g_len > 1500) {
     fprintf(stderr, "usage: queue_bench [producers] [packets_per_producer] [len 0..1500] [max_batch]\n");
     return 2;
+  }
+  /* every thread on the GPU's NUMA node (as numactl --cpunodebind would place a TransportManager's
+   * pools; QB_PIN=0: wherever the scheduler puts them), before the pinned rings are allocated */
+  const char* pin = getenv("QB_PIN");
+  const int node = wg_device_numa_node(0);
+  cpu_set_t set;
+  pthread_attr_t attr;
+  pthread_attr_init(&attr);
+  int pinned = -1;
+  if ((!pin || atoi(pin) != 0) && node_cpus(node, &set)) {
+    pthread_attr_setaffinity_np(&attr, sizeof set, &set);
+    pthread_setaffinity_np(pthread_self(), sizeof set, &set);
+    pinned = node;
   }
   if (wg_ctx_create(0, KEYS, &g_ctx) != WG_OK) {
     fprintf(stderr, "wg_ctx_create: %s\n", wg_last_error());
@@ -211,9 +250,9 @@ int main(int argc, char** argv) {
   throttled(&thp0, &thu0);
   const double cpu0 = cpu_seconds();
   const uint64_t t0 = now_ns();
-  for (int k = 0; k < nf; ++k) pthread_create(&th[g_P + k], NULL, forwarder, NULL);
-  for (int k = 0; k < nv; ++k) pthread_create(&th[g_P + nf + k], NULL, verifier, NULL);
-  for (int t = 0; t < g_P; ++t) pthread_create(&th[t], NULL, producer, (void*)(intptr_t)t);
+  for (int k = 0; k < nf; ++k) pthread_create(&th[g_P + k], &attr, forwarder, NULL);
+  for (int k = 0; k < nv; ++k) pthread_create(&th[g_P + nf + k], &attr, verifier, NULL);
+  for (int t = 0; t < g_P; ++t) pthread_create(&th[t], &attr, producer, (void*)(intptr_t)t);
   for (int t = 0; t < g_P; ++t) pthread_join(th[t], NULL);
   const double t_submit = (now_ns() - t0) * 1e-9;
   for (int k = 0; k < nf; ++k) pthread_join(th[g_P + k], NULL);
@@ -236,12 +275,12 @@ int main(int argc, char** argv) {
          "\"seal_lat_us\": {\"p50\": %.1f, \"p99\": %.1f, \"p999\": %.1f, \"max\": %.1f}, "
          "\"open_lat_us\": {\"p50\": %.1f, \"p99\": %.1f, \"p999\": %.1f, \"max\": %.1f}, "
          "\"seal_batches\": %llu, \"seal_mean_batch\": %.1f, \"open_batches\": %llu, \"open_mean_batch\": %.1f, "
-         "\"cpu_s\": %.3f, \"cpus_busy\": %.2f, \"throttled_periods\": %llu, \"throttled_ms\": %.1f}\n",
+         "\"cpu_s\": %.3f, \"cpus_busy\": %.2f, \"throttled_periods\": %llu, \"throttled_ms\": %.1f, \"pinned_node\": %d}\n",
          g_P, nf, nv, (unsigned long long)g_total, g_len ? argv[3] : "mixed 64..1500", max_batch,
          (unsigned long long)g_bad, wall, 2.0 * bytes / wall / gib, bytes / t_sealed / gib, bytes / t_submit / gib,
          g_total / wall, ls[0], ls[1], ls[2], ls[3], lo[0], lo[1], lo[2], lo[3], (unsigned long long)bs,
          bs ? (double)ps / bs : 0.0, (unsigned long long)bo, bo ? (double)po / bo : 0.0, cpu, cpu / wall,
-         thp1 - thp0, (thu1 - thu0) * 1e-3);
+         thp1 - thp0, (thu1 - thu0) * 1e-3, pinned);
   wg_queue_destroy(g_qs);
   wg_queue_destroy(g_qo);
   wg_ctx_destroy(g_ctx);

@@ -102,6 +102,7 @@ SIGNATURES = [
     ("wg_sync", _I, [_VP, _VP]),
     ("wg_last_error", ctypes.c_char_p, []),
     ("wg_version", ctypes.c_char_p, []),
+    ("wg_device_numa_node", _I, [_I]),
     ("wg_ctx_set_kernel", ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32]),
     ("wg_keys_set", _I, [_VP, _U32, _U32, _VP]),
     ("wg_keys_zero", _I, [_VP, _U32, _U32]),

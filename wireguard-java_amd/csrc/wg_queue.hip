@@ -139,6 +139,31 @@ struct Batch {  // one in-flight launch
   uint32_t n = 0;
 };
 
+// The CPUs of NUMA node `node` (sysfs cpulist "0-63,128-191"); false if unreadable.
+inline bool node_cpus(int node, cpu_set_t* set) {
+  if (node < 0) return false;
+  char path[96];
+  snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+  FILE* f = fopen(path, "r");
+  if (!f) return false;
+  char buf[4096];
+  const bool ok = fgets(buf, sizeof buf, f) != nullptr;
+  fclose(f);
+  if (!ok) return false;
+  CPU_ZERO(set);
+  int n = 0;
+  for (char* p = buf; *p && *p != '\n';) {
+    char* e;
+    const long a = strtol(p, &e, 10);
+    if (e == p) break;
+    long b = a;
+    if (*e == '-') b = strtol(e + 1, &e, 10);
+    for (long c = a; c <= b && c < CPU_SETSIZE; ++c, ++n) CPU_SET((int)c, set);
+    p = *e == ',' ? e + 1 : e;
+  }
+  return n > 0;
+}
+
 inline uint64_t now_ns() {
   return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
              std::chrono::steady_clock::now().time_since_epoch())
@@ -419,6 +444,20 @@ uint32_t pow2_at_least(uint32_t v) {
 
 extern "C" {
 
+int wg_device_numa_node(int device) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, (int)sizeof bus, device) != hipSuccess) return -1;
+  for (char* p = bus; *p; ++p) *p = (char)tolower(*p);
+  char path[160];
+  snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+  FILE* f = fopen(path, "r");
+  if (!f) return -1;
+  int node = -1;
+  if (fscanf(f, "%d", &node) != 1) node = -1;
+  fclose(f);
+  return node;
+}
+
 int wg_queue_create(wg_ctx* c, int mode, uint32_t capacity, uint32_t max_len, uint32_t max_batch, wg_queue** out) {
   if (!c || !out) return fail(WG_EINVAL, "NULL argument");
   *out = nullptr;
@@ -488,6 +527,12 @@ int wg_queue_create(wg_ctx* c, int mode, uint32_t capacity, uint32_t max_len, ui
   }
   wg_queue* qp = q.release();
   qp->disp = std::thread(queue_dispatch, qp);
+  // the dispatcher on the device's NUMA node (WG_QUEUE_PIN=0: wherever the scheduler puts it): on
+  // a two-socket host the far socket halved the harness's rate in some runs
+  const char* pin = getenv("WG_QUEUE_PIN");
+  cpu_set_t set;
+  if ((!pin || atoi(pin) != 0) && wgq::node_cpus(wg_device_numa_node(c->device), &set))
+    (void)pthread_setaffinity_np(qp->disp.native_handle(), sizeof set, &set);
   *out = qp;
   return WG_OK;
 }
