@@ -255,7 +255,11 @@ def test_held_caller_delays_nobody():
     print(j)
     assert j["failures"] == 0 and j["held_rc"] == 0
     assert j["held_us"] >= 50000
-    assert j["lat_us"]["max"] < 2000, j["lat_us"]
+    assert j["lat_us"]["p999"] < 2000, j["lat_us"]
+    # the max, too, unless the box's CPU quota stalled the whole process meanwhile (17 busy threads
+    # on 16 CPUs of quota): then still far below the 50 ms a blocked wave would add
+    bound = 2000 if j["throttled_periods"] == 0 else 20000
+    assert j["lat_us"]["max"] < bound, (j["lat_us"], j["throttled_periods"])
 
 
 @pytest.mark.gpu
@@ -292,3 +296,16 @@ def test_batcher_entry_points_reject_bad_arguments():
     assert lib.wg_batcher_config(None, 16, 0) == E
     assert lib.wg_pp_config(None, 16, 0) == E
     assert lib.wg_batcher_stats(None, None, None) == E
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("callers", [64, 128])
+def test_more_callers_than_cpus_tail_latency(callers):
+    """More synchronous callers than the CPUs the process may use (the GPU box: 16 CPUs of cgroup
+    quota): only that many poll for their completion, the rest sleep on a futex, so the process
+    never exhausts its quota and no call waits out a throttled period (polling callers had p999
+    74 / 88 ms at 64 / 128)."""
+    j = _batcher_bench(callers, 160000 // callers, 1420)
+    print(j)
+    assert j["failures"] == 0
+    assert j["lat_us"]["p999"] < 2000, (j["lat_us"], j["throttled_periods"])

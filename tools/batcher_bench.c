@@ -94,6 +94,19 @@ static int cmpd(const void* a, const void* b) {
   return x < y ? -1 : x > y;
 }
 
+/* the cgroup's throttled periods (cgroup v2 cpu.stat), 0 where absent: the GPU box allows the
+ * process 16 CPUs of time while it may run on all of them */
+static unsigned long long throttled_periods(void) {
+  FILE* f = fopen("/sys/fs/cgroup/cpu.stat", "r");
+  if (!f) return 0;
+  char k[64];
+  unsigned long long v, r = 0;
+  while (fscanf(f, "%63s %llu", k, &v) == 2)
+    if (!strcmp(k, "nr_throttled")) r = v;
+  fclose(f);
+  return r;
+}
+
 int main(int argc, char** argv) {
   const int T = argc > 1 ? atoi(argv[1]) : 16;
   g_calls = argc > 2 ? atoi(argv[2]) : 10000;
@@ -153,6 +166,7 @@ int main(int argc, char** argv) {
   }
   uint64_t l0 = 0, p0 = 0;
   wg_batcher_stats(g_ctx, &l0, &p0);
+  const unsigned long long thr0 = throttled_periods();
   double t0 = now_us();
   pthread_t hth;
   if (hold_us) pthread_create(&hth, NULL, held, NULL);
@@ -160,6 +174,7 @@ int main(int argc, char** argv) {
   for (int t = 0; t < T; ++t) pthread_join(th[t], NULL);
   if (hold_us) pthread_join(hth, NULL);
   double wall = now_us() - t0;
+  const unsigned long long thr1 = throttled_periods();
   uint64_t l1 = 0, p1 = 0;
   wg_batcher_stats(g_ctx, &l1, &p1);
   size_t n = (size_t)T * g_calls;
@@ -174,12 +189,12 @@ int main(int argc, char** argv) {
          "\"calls\": %zu, \"failures\": %d, \"wall_s\": %.4f, \"calls_per_s\": %.0f, "
          "\"payload_gib_s\": %.4f, \"lat_us\": {\"p50\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"p999\": %.1f, "
          "\"max\": %.1f}, \"launches\": %llu, \"mean_batch\": %.1f, \"gap_us\": %d, \"waves\": %d, "
-         "\"fail_launches\": %d, \"hold_us\": %d, \"held_us\": %.1f, \"held_rc\": %d}\n",
+         "\"fail_launches\": %d, \"hold_us\": %d, \"held_us\": %.1f, \"held_rc\": %d, \"throttled_periods\": %llu}\n",
          T, g_calls, g_len ? argv[3] : "mixed 64..1500", n, fails, wall * 1e-6, n / (wall * 1e-6),
          bytes / (wall * 1e-6) / (double)(1u << 30), g_lat[n / 2], g_lat[n * 9 / 10], g_lat[n * 99 / 100],
          g_lat[n * 999 / 1000], g_lat[n - 1], (unsigned long long)(l1 - l0),
          (l1 > l0) ? (double)(p1 - p0) / (double)(l1 - l0) : 0.0, g_gap_us, waves, fail_launches, hold_us,
-         g_held_us, g_held_rc);
+         g_held_us, g_held_rc, thr1 - thr0);
   wg_ctx_destroy(g_ctx);
   return (fails || g_held_rc) ? 1 : 0;
 }
