@@ -10,6 +10,7 @@
 #include <linux/futex.h>
 #include <pthread.h>
 #include <sched.h>
+#include <sys/prctl.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 

@@ -244,6 +244,9 @@ void queue_complete(wg_queue* q, wgq::Batch& b, uint32_t status_override) {
 
 void queue_dispatch(wg_queue* q) {
   DeviceGuard g(q->c->device);
+  // short naps below (a few us) must not be stretched to the default 50-us timer slack
+  (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
+  uint32_t idle = 0;  // loop turns without a completion, a gathered packet or a launch
   uint32_t next = 0, oldest = 0, live = 0;  // batch ring: `live` in flight from `oldest`
   uint32_t rr = 0;                          // lane the next gather starts at
   wgq::Batch* fill = &q->batches[next];
@@ -262,6 +265,7 @@ void queue_dispatch(wg_queue* q) {
       queue_complete(q, b, e == hipSuccess ? 0u : (uint32_t)WG_PKT_FAILED);
       oldest = (oldest + 1u) % q->inflight;
       --live;
+      idle = 0;
     }
     // gather ready packets into the batch being filled
     if (live < q->inflight) {
@@ -286,7 +290,10 @@ void queue_dispatch(wg_queue* q) {
         ln.r_head.store(h, std::memory_order_relaxed);
       }
       rr = (rr + 1) % q->lanes;
-      if (taken) q->ready_hint.fetch_sub(taken, std::memory_order_relaxed);
+      if (taken) {
+        q->ready_hint.fetch_sub(taken, std::memory_order_relaxed);
+        idle = 0;
+      }
       // launch once min_batch packets wait, or when the first of them has waited window_ns (a light
       // load: one packet waits at most that long; a heavy one fills batches of min_batch and more)
       if (fill->n > 0 && (fill->n >= q->min_batch || wgq::now_ns() - first_ns >= q->window_ns)) {
@@ -305,7 +312,11 @@ void queue_dispatch(wg_queue* q) {
     }
     if (q->quit.load(std::memory_order_acquire) && live == 0 && fill->n == 0) break;
     if (live > 0 || fill->n > 0) {
-      std::this_thread::yield();  // a batch runs or one is filling: poll the events and the ready queue
+      // a batch runs or one is filling: poll the events and the ready lanes; after 32 idle turns in a
+      // row nap 4 us between polls (a dispatcher that only yields keeps a core busy for the whole
+      // time a batch runs, and on a CPU quota that core is one the producers and consumers lack)
+      if (++idle > 32u) std::this_thread::sleep_for(std::chrono::microseconds(4));
+      else std::this_thread::yield();
       continue;
     }
     // nothing in flight and nothing ready: sleep until a producer pushes (or 1 ms)
