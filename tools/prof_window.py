@@ -33,7 +33,9 @@ def bench_line(path):
 
 
 def window(b):
-    per = b["roofline"].get("launches_per_step", 1)
+    # a K-stream step (bench.py --streams K > 1) cuts the batch into K runs, one launch each
+    st = b["roofline"].get("step") or {}
+    per = st["launches"] if st.get("streams", 1) > 1 else b["roofline"].get("launches_per_step", 1)
     skip = (b["ramp_steps"] + b["warmup"] + b.get("graph_warm_steps", 0)) * per
     return skip, b["steps"] * per, per
 
@@ -79,18 +81,27 @@ def trace(args):
                         "max_us": round(max(v), 3), "median_us": round(sorted(v)[len(v) // 2], 3)}
                     for k, v in sorted(per_kernel.items())},
     }
-    alg = b["roofline"]["alg_bytes_per_launch"] * per  # per step
+    st = b["roofline"].get("step") or {}
+    multi = st.get("streams", 1) > 1
+    # per step: a K-stream step's K launches together move one batch (the one-stream kernel's bytes)
+    alg = b["roofline"]["alg_bytes_per_launch"] * (b["roofline"].get("launches_per_step", 1) if multi else per)
+    if multi:  # compare with the K-stream step's own fraction, not the one-stream kernel's
+        out["bench_frac"] = st["frac"]
+        out["streams"] = st["streams"]
     # the bench's frac is bytes per step over the device time of a step (HIP events around the
     # whole timed region): the profile's counterpart is the window's span per step (launches of
     # one step may overlap on two streams, so their summed durations can exceed it)
     out["frac_from_profile"] = round(alg / (span_us / b["steps"] * 1e-6) / 8.0e12, 4)
-    out["frac_vs_bench"] = round(out["frac_from_profile"] / b["roofline"]["frac"], 4)
+    out["frac_vs_bench"] = round(out["frac_from_profile"] / out["bench_frac"], 4)
     out["span_le_bench_ms_per_step"] = span_us / b["steps"] * 1e-3 <= b["ms_per_step"]
     # the same fraction from the kernels' own durations: under rocprofv3 the host can take longer to
     # enqueue a step than the GPU takes to run it (the profiler intercepts every dispatch), and
     # then the span holds idle gaps that the unprofiled bench does not have
     out["frac_from_kernel_time"] = round(alg / (busy_us / b["steps"] * 1e-6) / 8.0e12, 4)
-    out["host_bound_under_profiler"] = span_us > 1.05 * busy_us
+    # K streams overlap their launches: the summed durations exceed the span, so only the span says
+    # whether the host kept the device fed
+    out["host_bound_under_profiler"] = span_us > 1.05 * busy_us if not multi else \
+        span_us / b["steps"] * 1e-3 > 1.05 * b["ms_per_step"]
     return out
 
 
