@@ -29,7 +29,12 @@ The JSON line also carries:
                 against the 8 TB/s HBM peak: achieved = sum(4L + 32) per step / GPU time per step
                 (SURVEY.md §8d), GPU time from HIP events on the launch stream around
                 the timed region; `traffic` = HBM bytes per launch from the committed
-                rocprofv3 PMC summary (profiles/pmc_*.json) when present
+                rocprofv3 PMC summary (profiles/pmc_*.json) when present.
+                Steps on K > 1 streams (--streams; default 2 for uniform workloads): the batch is
+                cut into K runs whose launches overlap, so a launch's duration says nothing about
+                the kernel; `roofline` is then the one-stream kernel, the same steps re-timed on
+                one stream right after the timed region (`kernel_ms`, one launch per step), and
+                `roofline.step` the timed K-stream steps (`value` comes from those)
   cpu_baseline  the CPU restatement (oracle/liboracle.so, bit-exact to the
                 reference) timed on this host's cores, rank 0, N = 1 only
   oracle_sample ct||tag of 2048 seeded packets of the timed batch against the oracle (rank 0,
