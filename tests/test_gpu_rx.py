@@ -184,18 +184,17 @@ def test_reference_filter_known_answers_on_device(engine):
     assert got == [rx.PKT_OK, rx.PKT_FILTERED, rx.PKT_OK, rx.PKT_FILTERED]  # IPFilter.java:85-88
 
 
-@pytest.fixture(params=["four_launches", "five_launches"])
-def rp_engine(request, engine):
-    """An engine whose replay checks run in four launches (order, insert, decide + advance, mark) or
-    with decide and advance launched separately (WG_RX_LAUNCHES=5, read when the context's receive
-    state is created)."""
+@pytest.fixture(params=["three_launches", "four_launches", "five_launches"])
+def rp_engine(request):
+    """An engine whose replay checks take each launch structure: three launches (judge with the
+    windows advanced by its last block, insert, fix-up + mark; at most 512 key slots), four (the
+    same with a separate advance launch; more than 512 key slots), or the five-launch path
+    (WG_RX_LAUNCHES=5, read when the context's receive state is created)."""
     import os
     old = os.environ.get("WG_RX_LAUNCHES")
-    os.environ["WG_RX_LAUNCHES"] = "4" if request.param == "four_launches" else "5"
+    os.environ["WG_RX_LAUNCHES"] = "5" if request.param == "five_launches" else "3"
     try:
-        # at most 512 key slots: the last block of k_rp_decide_adv advances them (larger tables launch
-        # k_rp_advance whatever WG_RX_LAUNCHES says)
-        e = wg().Engine(0, key_slots=512)
+        e = wg().Engine(0, key_slots=1024 if request.param == "four_launches" else 512)
         e.replay_enable(64)
     finally:
         if old is None:
@@ -282,7 +281,7 @@ def test_replay_sorted_batches_match_oracle(rp_engine):
 @pytest.mark.parametrize("sorted_batch", [False, True])
 def test_replay_large_batches_many_slots(rp_engine, sorted_batch):
     """Batches of 300,000 packets over 512 key slots (1,172 blocks racing to be the last of
-    k_rp_decide_adv, every slot's new top spread over 8 copies): interleaved slots (the table path,
+    k_rp_judge, every slot's new top spread over 8 copies): interleaved slots (the table path,
     with duplicates) or the same packets sorted by (slot, counter) (no table)."""
     engine = rp_engine
     torch, dev = _dev()

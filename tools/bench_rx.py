@@ -4,8 +4,8 @@ with a 3-prefix AllowedIPs filter), after a 150-ms clock ramp:
   wg_rx_check alone: filter, replay, both; replay over 1024 key slots.
 HIP events on the launch stream around each of 200 calls (open variants: 200 calls each,
 alternating between the variants); the replay window is re-enabled (emptied, untimed) before each
-replay call so every call sees fresh counters. WG_RX_LAUNCHES=5 times the replay path with decide
-and advance as separate launches (the default runs the advance in the decide launch's last block)."""
+replay call so every call sees fresh counters. WG_RX_LAUNCHES=5 times the five-launch replay path
+(the default: three launches for tables of at most 512 key slots, four above)."""
 import json
 import os
 import sys
@@ -34,7 +34,7 @@ def main():
     dpt = torch.from_numpy(pt.reshape(-1)).to(dev)
     st0 = torch.zeros(n, dtype=torch.int32, device=dev)
     st = st0.clone()
-    out = {"n": n, "rx_launches": 5 if os.environ.get("WG_RX_LAUNCHES") == "5" else 4}
+    out = {"n": n, "rx_launches": 5 if os.environ.get("WG_RX_LAUNCHES") == "5" else 3}
     eng.set_keys(0, bytes(range(32)))
     ct = torch.zeros_like(dpt)
     back = torch.zeros_like(dpt)

@@ -6,7 +6,7 @@ mkdir -p $out
 timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_rx.py -m gpu > $out/tests.log 2>&1 || { tail -40 $out/tests.log; exit 1; }
 tail -3 $out/tests.log
 for k in 1 2; do
-  for f in 4 5; do
+  for f in 3 5; do
     WG_RX_LAUNCHES=$f timeout -k 10 200 python tools/bench_rx.py >> $out/rx.jsonl 2>>$out/err || exit 1
   done
 done

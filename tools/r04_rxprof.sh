@@ -4,7 +4,7 @@
 set -o pipefail
 out=gpurun_out/${1:-r04rp}
 mkdir -p $out
-for f in 4 5; do
+for f in 3 5; do
   WG_RX_LAUNCHES=$f timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/f$f -o run --output-format csv -- python3 tools/bench_rx.py > $out/f$f.log 2>&1 || { tail -20 $out/f$f.log; exit 1; }
   grep '^{' $out/f$f.log | tail -1
   python3 - $out/f$f <<'PY'
@@ -21,7 +21,7 @@ for k, v in dur.items():
 calls, cur = [], []
 for r in rows:
     n = r['Kernel_Name']
-    if ('k_rp_order' in n) and cur:
+    if ('k_rp_order' in n or 'k_rp_judge' in n) and cur:
         calls.append(cur); cur = []
     cur.append(r)
 if cur: calls.append(cur)

@@ -34,9 +34,11 @@
 // ever accepted twice. oracle/rx.py restates these rules one packet at a time.
 // Kernels: k_rp_order flags a batch whose (slot, counter) pairs do not strictly increase with
 // the index (only then can a pair repeat); k_rp_insert claims one entry per (slot, counter) pair in an open-addressing table
-// (lowest index by atomicMin), k_rp_decide_adv judges against the old window and its last block
-// moves each slot's window (k_rp_decide + k_rp_advance for tables of more than 512 slots),
-// k_rp_mark sets the ring bits and empties the table again. Atomics on a shared address (a
+// (lowest index by atomicMin). By default k_rp_judge raises the flag and judges every packet against
+// the old window as if no pair repeated (its last block then moves each slot's window; a separate
+// k_rp_advance for tables of more than 512 slots), k_rp_insert fills the table only for a flagged
+// batch, and k_rp_fixmark turns every copy of a repeated pair but the lowest into REPLAY, sets the
+// ring bits and empties the table again. Atomics on a shared address (a
 // slot's new top, a window word) are aggregated per workgroup first; new tops are spread over 8
 // copies per slot.
 #pragma once
@@ -47,7 +49,7 @@ constexpr uint32_t kRxNoFilter = 0xFFFFFFFFu;
 constexpr uint64_t kRejectAfter = ~0ull - 8191ull - 1ull;  // 2^64 - 2^13 - 1
 constexpr uint64_t kEmptyKey = ~0ull;                      // counters that large are rejected first
 constexpr uint32_t kTopWays = 8;         // copies of each slot's new top (spread same-address atomics)
-// key slots the last block of k_rp_decide_adv advances: one peer's 64K packets in order 25 us per
+// key slots the last block of k_rp_judge advances: one peer's 64K packets in order 25 us per
 // check against 31 as separate launches, but 1024 interleaved slots 65 against 60 (the last block
 // walks every slot), so larger tables launch the advance (profiles/r04_rx_launches.txt)
 constexpr uint32_t kAdvanceInline = 512;
@@ -65,7 +67,7 @@ struct RxState {
   DevBuf d_tab;             // (slot, counter) -> lowest batch index, open addressing; all empty between calls
   uint32_t tab_size = 0;    // entries (a power of two >= 2n)
   DevBuf d_pos;             // per packet: its (slot, counter) entry in d_tab, or ~0
-  DevBuf d_flag;            // {k_rp_order's flag, k_rp_decide_adv's finished blocks} (0 between calls)
+  DevBuf d_flag;            // {the order flag, k_rp_judge's finished blocks} (0 between calls)
   bool five = false;        // WG_RX_LAUNCHES=5: decide and advance as two launches (A/B)
   hipEvent_t ev = nullptr;  // last use of the replay scratch, and its stream (stream-ordered reuse)
   hipStream_t ev_stream = (hipStream_t)-1;
@@ -206,7 +208,7 @@ struct RxParams {
   uint32_t tab_size;
   uint32_t* pos;
   uint32_t* unsorted;  // 0 while the batch's (slot, counter) pairs strictly increase with the index
-  uint32_t* done_blocks;  // k_rp_decide_adv: blocks finished (0 between calls)
+  uint32_t* done_blocks;  // k_rp_judge: blocks finished (0 between calls)
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -390,7 +392,7 @@ __device__ __forceinline__ void rp_decide_at(const RxParams& P, uint32_t i, bool
 }
 
 // per slot: the window moves to newtop (the largest of its kTopWays copies, read as device-scope
-// atomics: in k_rp_decide_adv the last block reads what every block raised); ring positions of the
+// atomics: in k_rp_judge the last block reads what every block raised); ring positions of the
 // counters it passed are cleared and every copy is set to the new top again
 __device__ __forceinline__ void rp_advance_to(const RxParams& P, uint32_t slot, uint64_t top, uint64_t nt) {
   const uint32_t W = P.window, words = W / 64;
@@ -429,7 +431,7 @@ __device__ __forceinline__ void rp_advance_at(const RxParams& P, uint32_t slot) 
 // accepted counters still inside the advanced window get their ring bit; the table entries this
 // batch used are emptied again (nothing reads the table in this phase). Every thread of the block
 // calls it (block_group).
-__device__ __forceinline__ void rp_mark_at(const RxParams& P, uint32_t i) {
+__device__ __forceinline__ void rp_mark_at(const RxParams& P, uint32_t i, bool clean = true) {
   uint32_t slot = 0;
   uint64_t c = 0;
   bool act = i < P.n && rp_candidate(P, i, slot, c);  // accepted packets are still OK
@@ -439,35 +441,14 @@ __device__ __forceinline__ void rp_mark_at(const RxParams& P, uint32_t i) {
   block_group<false, true>(act, word, 1ull << (pos % 64), [&](uint64_t k, uint64_t, uint64_t orv) {
     atomicOr((unsigned long long*)&P.bits[k], (unsigned long long)orv);
   });
-  if (i < P.n && P.pos[i] != ~0u) P.tab[P.pos[i]] = ~0u;
+  if (clean && i < P.n && P.pos[i] != ~0u) P.tab[P.pos[i]] = ~0u;
 }
 
-// The phases as launches: k_rp_order | k_rp_insert (skipped for a strictly increasing batch) |
-// k_rp_decide_adv (its last block to finish advances every slot's window) | k_rp_mark. Tables of
-// more than kAdvanceInline key slots (and WG_RX_LAUNCHES=5, for A/B) take k_rp_decide +
-// k_rp_advance instead of k_rp_decide_adv. (Inserting every pair to drop the order check made the
-// insert 21 us instead of 3: the table's CAS-with-return round trips cost more than a launch.)
-__global__ void __launch_bounds__(256) k_rp_order(RxParams P) { rp_order_at(P, blockIdx.x * 256u + threadIdx.x); }
-__global__ void __launch_bounds__(256) k_rp_insert(RxParams P) {
-  rp_insert_at(P, blockIdx.x * 256u + threadIdx.x, *P.unsorted != 0);
-}
-__global__ void __launch_bounds__(256) k_rp_decide(RxParams P) {
-  rp_decide_at(P, blockIdx.x * 256u + threadIdx.x, *P.unsorted != 0);
-}
-__global__ void __launch_bounds__(256) k_rp_advance(RxParams P) { rp_advance_at(P, blockIdx.x * 256u + threadIdx.x); }
-__global__ void __launch_bounds__(256) k_rp_decide_adv(RxParams P) {
-  rp_decide_at(P, blockIdx.x * 256u + threadIdx.x, *P.unsorted != 0);
-  // every atomicMax of this block has completed before the block counts itself done, so the last
-  // block's device-scope loads see every block's new tops (no cache flush needed)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// The last block of a launch advances every slot's window (tables of at most kAdvanceInline slots).
+__device__ __forceinline__ void rp_advance_all(const RxParams& P) {
+  __shared__ uint32_t nfull, full[64];
+  if (threadIdx.x == 0) nfull = 0;
   __syncthreads();
-  __shared__ uint32_t last, nfull, full[64];
-  if (threadIdx.x == 0) {
-    last = atomicAdd(P.done_blocks, 1u) == gridDim.x - 1u;
-    nfull = 0;
-  }
-  __syncthreads();
-  if (!last) return;
   // a slot whose window moves by W or more has every word cleared: by the whole block (a batch of
   // one peer's 64K packets clears 128 words), listed here; every other advance runs per thread
   const uint32_t words = P.window / 64;
@@ -512,7 +493,59 @@ __global__ void __launch_bounds__(256) k_rp_decide_adv(RxParams P) {
     uint64_t* b = P.bits + (uint64_t)full[f] * words;
     for (uint32_t k = threadIdx.x; k < words; k += 256u) b[k] = 0;
   }
-  if (threadIdx.x == 0) *P.done_blocks = 0u;  // for the next check (the kernel boundary orders it)
+}
+
+// Counts the calling block done once every atomic it issued has completed; true in the last block
+// of the grid (whose device-scope loads then see every block's new tops; no cache flush needed).
+__device__ __forceinline__ bool rp_last_block(const RxParams& P) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ uint32_t last;
+  if (threadIdx.x == 0) last = atomicAdd(P.done_blocks, 1u) == gridDim.x - 1u;
+  __syncthreads();
+  return last;
+}
+
+// The phases as launches. Default: k_rp_judge (order flag + decisions without the table; its last
+// block advances the windows for tables of at most kAdvanceInline slots, else k_rp_advance follows)
+// | k_rp_insert (a no-op for a strictly increasing batch) | k_rp_fixmark. WG_RX_LAUNCHES=5 (A/B):
+// k_rp_order | k_rp_insert | k_rp_decide | k_rp_advance | k_rp_mark. (Inserting every pair to drop
+// the order check made the insert 21 us instead of 3: the table's CAS-with-return round trips cost
+// more than a launch.)
+__global__ void __launch_bounds__(256) k_rp_order(RxParams P) { rp_order_at(P, blockIdx.x * 256u + threadIdx.x); }
+__global__ void __launch_bounds__(256) k_rp_insert(RxParams P) {
+  rp_insert_at(P, blockIdx.x * 256u + threadIdx.x, *P.unsorted != 0);
+}
+__global__ void __launch_bounds__(256) k_rp_decide(RxParams P) {
+  rp_decide_at(P, blockIdx.x * 256u + threadIdx.x, *P.unsorted != 0);
+}
+__global__ void __launch_bounds__(256) k_rp_advance(RxParams P) { rp_advance_at(P, blockIdx.x * 256u + threadIdx.x); }
+// The default path's first launch: the order flag, and the decisions as if no (slot, counter) pair
+// repeated (a repeated pair's copies all get the same verdict against the old window, and the
+// same new top); k_rp_fixmark turns every copy but the lowest into REPLAY when the flag is up.
+// With `advance` its last block moves every slot's window.
+__global__ void __launch_bounds__(256) k_rp_judge(RxParams P, uint32_t advance) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  rp_order_at(P, i);
+  rp_decide_at(P, i, false);
+  if (!advance || !rp_last_block(P)) return;
+  rp_advance_all(P);
+  if (threadIdx.x == 0) *P.done_blocks = 0u;
+}
+// After k_rp_insert (a no-op for a strictly increasing batch): copies of a pair other than its
+// lowest index become REPLAY, then the ring bits of the accepted counters; each used table entry is
+// emptied by its lowest index only, after that thread has read it (another copy reading it emptied
+// still finds an index other than its own)
+__global__ void __launch_bounds__(256) k_rp_fixmark(RxParams P) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  bool own_entry = false;
+  if (*P.unsorted && i < P.n && P.pos[i] != ~0u) {
+    own_entry = P.tab[P.pos[i]] == i;
+    if (!own_entry && P.status[i] == WG_PKT_OK) P.status[i] = WG_PKT_REPLAY;
+  }
+  rp_mark_at(P, i, false);
+  if (own_entry) P.tab[P.pos[i]] = ~0u;
+  if (i == 0) *P.unsorted = 0u;  // every reader of the flag ran before this launch
 }
 __global__ void __launch_bounds__(256) k_rp_mark(RxParams P) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
@@ -712,15 +745,20 @@ int wg_rx_check(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* pt, ui
     P.pos = (uint32_t*)r->d_pos.p;
     P.unsorted = (uint32_t*)r->d_flag.p;
     P.done_blocks = (uint32_t*)r->d_flag.p + 1;
-    hipLaunchKernelGGL(wgrx::k_rp_order, dim3(grid), dim3(256), 0, s, P);
-    hipLaunchKernelGGL(wgrx::k_rp_insert, dim3(grid), dim3(256), 0, s, P);
-    if (!r->five && c->key_slots <= kAdvanceInline) {
-      hipLaunchKernelGGL(wgrx::k_rp_decide_adv, dim3(grid), dim3(256), 0, s, P);
+    if (!r->five) {
+      const bool inl = c->key_slots <= kAdvanceInline;
+      hipLaunchKernelGGL(wgrx::k_rp_judge, dim3(grid), dim3(256), 0, s, P, inl ? 1u : 0u);
+      if (!inl)
+        hipLaunchKernelGGL(wgrx::k_rp_advance, dim3((c->key_slots + 255u) / 256u), dim3(256), 0, s, P);
+      hipLaunchKernelGGL(wgrx::k_rp_insert, dim3(grid), dim3(256), 0, s, P);
+      hipLaunchKernelGGL(wgrx::k_rp_fixmark, dim3(grid), dim3(256), 0, s, P);
     } else {
+      hipLaunchKernelGGL(wgrx::k_rp_order, dim3(grid), dim3(256), 0, s, P);
+      hipLaunchKernelGGL(wgrx::k_rp_insert, dim3(grid), dim3(256), 0, s, P);
       hipLaunchKernelGGL(wgrx::k_rp_decide, dim3(grid), dim3(256), 0, s, P);
       hipLaunchKernelGGL(wgrx::k_rp_advance, dim3((c->key_slots + 255u) / 256u), dim3(256), 0, s, P);
+      hipLaunchKernelGGL(wgrx::k_rp_mark, dim3(grid), dim3(256), 0, s, P);
     }
-    hipLaunchKernelGGL(wgrx::k_rp_mark, dim3(grid), dim3(256), 0, s, P);
     const hipError_t le = hipGetLastError();
     if (le != hipSuccess) {
       r->tab_size = 0;  // the table / flag may be left dirty: the next check starts from empty ones
