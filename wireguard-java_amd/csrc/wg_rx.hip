@@ -49,6 +49,7 @@ constexpr uint32_t kRxNoFilter = 0xFFFFFFFFu;
 constexpr uint64_t kRejectAfter = ~0ull - 8191ull - 1ull;  // 2^64 - 2^13 - 1
 constexpr uint64_t kEmptyKey = ~0ull;                      // counters that large are rejected first
 constexpr uint32_t kTopWays = 8;         // copies of each slot's new top (spread same-address atomics)
+constexpr size_t kFlagBytes = 64 * (2 + kTopWays);  // order flag | done count | kTopWays group counts
 // key slots the last block of k_rp_judge advances: one peer's 64K packets in order 25 us per
 // check against 31 as separate launches, but 1024 interleaved slots 65 against 60 (the last block
 // walks every slot), so larger tables launch the advance (profiles/r04_rx_launches.txt)
@@ -67,7 +68,7 @@ struct RxState {
   DevBuf d_tab;             // (slot, counter) -> lowest batch index, open addressing; all empty between calls
   uint32_t tab_size = 0;    // entries (a power of two >= 2n)
   DevBuf d_pos;             // per packet: its (slot, counter) entry in d_tab, or ~0
-  DevBuf d_flag;            // {the order flag, k_rp_judge's finished blocks} (0 between calls)
+  DevBuf d_flag;            // the order flag, k_rp_judge's finished blocks and groups, 64 B apart (0 between calls)
   bool five = false;        // WG_RX_LAUNCHES=5: decide and advance as two launches (A/B)
   hipEvent_t ev = nullptr;  // last use of the replay scratch, and its stream (stream-ordered reuse)
   hipStream_t ev_stream = (hipStream_t)-1;
@@ -497,11 +498,22 @@ __device__ __forceinline__ void rp_advance_all(const RxParams& P) {
 
 // Counts the calling block done once every atomic it issued has completed; true in the last block
 // of the grid (whose device-scope loads then see every block's new tops; no cache flush needed).
+// Two levels (kTopWays groups of blocks, then the groups): a counter that every block of a 256-block
+// grid raises serialises 256 same-address atomics; each counter sits on its own 64-B line.
 __device__ __forceinline__ bool rp_last_block(const RxParams& P) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   __shared__ uint32_t last;
-  if (threadIdx.x == 0) last = atomicAdd(P.done_blocks, 1u) == gridDim.x - 1u;
+  if (threadIdx.x == 0) {
+    const uint32_t groups = min(gridDim.x, kTopWays), g = blockIdx.x % groups;
+    const uint32_t members = (gridDim.x - g + groups - 1u) / groups;  // blocks b < grid with b % groups == g
+    uint32_t* gc = P.done_blocks + 16u * (1u + g);
+    last = false;
+    if (atomicAdd(gc, 1u) == members - 1u) {
+      *gc = 0u;  // every member has arrived: ready for the next check (the kernel boundary orders it)
+      last = atomicAdd(P.done_blocks, 1u) == groups - 1u;
+    }
+  }
   __syncthreads();
   return last;
 }
@@ -730,9 +742,9 @@ int wg_rx_check(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* pt, ui
       HIPTRY(hipDeviceSynchronize());  // the scratch is reallocated under earlier checks
     if (T > r->tab_size) {  // (re)allocated, or reset after a failed check: all entries empty
       if ((rc = r->d_tab.ensure((size_t)T * 4)) != WG_OK) return rc;
-      if ((rc = r->d_flag.ensure(8)) != WG_OK) return rc;
+      if ((rc = r->d_flag.ensure(kFlagBytes)) != WG_OK) return rc;
       HIPTRY(hipMemsetAsync(r->d_tab.p, 0xFF, (size_t)T * 4, s));
-      HIPTRY(hipMemsetAsync(r->d_flag.p, 0, 8, s));
+      HIPTRY(hipMemsetAsync(r->d_flag.p, 0, kFlagBytes, s));
       r->tab_size = T;
     }
     if ((rc = r->d_pos.ensure((size_t)n * 4)) != WG_OK) return rc;
@@ -744,7 +756,7 @@ int wg_rx_check(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* pt, ui
     P.tab_size = r->tab_size;
     P.pos = (uint32_t*)r->d_pos.p;
     P.unsorted = (uint32_t*)r->d_flag.p;
-    P.done_blocks = (uint32_t*)r->d_flag.p + 1;
+    P.done_blocks = (uint32_t*)r->d_flag.p + 16;  // its own line; group counters on the next lines
     if (!r->five) {
       const bool inl = c->key_slots <= kAdvanceInline;
       hipLaunchKernelGGL(wgrx::k_rp_judge, dim3(grid), dim3(256), 0, s, P, inl ? 1u : 0u);
