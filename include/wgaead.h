@@ -364,8 +364,12 @@ int wg_open_host(wg_ctx* ctx, const wg_pkt* desc_host, uint32_t n, const uint8_t
  *     pinned ring: ct || tag (len + 16 B) for a seal, the plaintext (len B, valid when status is
  *     WG_PKT_OK; WG_PKT_BADTAG: rejected, ChaCha20Poly1305.java:51-55) for an open. Completions
  *     come back in batch order, not in submission order.
- *   wg_reap_done(q, c, n): the consumer is done with these completions (their slots are reused).
- *   wg_queue_destroy: waits for the batches in flight; unreaped completions are dropped. */
+ *   wg_reap_done(q, c, n): the consumer is done with these completions (their slots are reused);
+ *     each completion exactly once (a slot handed back twice would be given to two producers).
+ *   wg_queue_destroy: waits for the batches in flight; unreaped completions are dropped. Call it
+ *     only once no thread is inside (or can still enter) wg_submit_* / wg_reap* on this queue.
+ * A producer thread keeps up to 32 slots taken from other lanes in its lane's stash; slots stashed
+ * by a thread that exits are used by the next thread that maps to the same lane. */
 #define WG_QUEUE_MAX_LEN 16384u
 typedef struct wg_queue wg_queue;
 typedef struct wg_completion {
