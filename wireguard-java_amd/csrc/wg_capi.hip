@@ -109,6 +109,9 @@ struct wg_ctx {
   uint32_t mixed_split = 0;               // > 0: mixed batches one packet per slot, packets of more than this
                                           // many 8-block rounds in 16-lane slots (WG_MIXED_SPLIT)
   bool step_two_launches = false;         // wg_ctx_set_kernel variant 1: WG_F_AFTER_SEAL as seal + open launches
+  // half-occupancy k_step grids (C2's longest-first pairs) take the build allocated for 4 waves per
+  // SIMD: no SGPR spills, C2 +0.7% in 3 alternations (profiles/r04_wpe_ab.txt); WG_STEP_WPE4=0: not
+  bool step_wpe4 = true;
   // plan workspace: k_tile block scan, k_transport longest-first order
   DevBuf plan_nb, plan_prefix, plan_tiles, plan_ntiles, plan_tmp, lpt_hist, lpt_order;
   DevBuf lpt_hist2, lpt_order2;  // the open half of a wg_duplex_batch
@@ -545,6 +548,8 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
       record_start(c, s, &ev);
       if (PS.n_long) hipLaunchKernelGGL(wgt::k_step_mixed, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else if (G == 16) hipLaunchKernelGGL(wgt::k_step<16>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+      else if (c->step_wpe4 && 2ull * gs * wgt::TW <= cap)
+        hipLaunchKernelGGL((wgt::k_step<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else hipLaunchKernelGGL(wgt::k_step<8>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       const hipError_t e = hipGetLastError();
       record_end(c, s, ev);
@@ -648,6 +653,7 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   if (const char* e = getenv("WG_MIXED_SPLIT")) c->mixed_split = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_UNIFORM16")) c->uniform16 = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_PRIO")) c->prio_mode = atoi(e);
+  if (const char* e = getenv("WG_STEP_WPE4")) c->step_wpe4 = atoi(e) != 0;
   *out = c;
   return WG_OK;
 }

@@ -807,8 +807,12 @@ k_duplex(TransportParams S, TransportParams O, uint32_t seal_blocks, uint32_t op
 // grid and one packet order, so slot g opens exactly the packets it sealed. The waves that finish
 // sealing first start opening while the others still seal: the seal launch's tail and the open
 // launch's start, which two back-to-back launches leave partly idle, overlap.
-template <int G = 8>
-__global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)))
+// WPE: the waves per SIMD the register allocation targets. 8 (64 VGPRs) everywhere, except a grid
+// that holds at most half the resident waves anyway (the persistent longest-first pairs of a
+// mixed batch: 4 waves per SIMD), which takes the WPE = 4 build (66 VGPRs and no SGPR spills,
+// against 64 VGPRs and 12 SGPRs spilled to VGPR lanes; WG_STEP_WPE4=0 for the other).
+template <int G = 8, int WPE = 8>
+__global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_step(TransportParams S, TransportParams O) {
   __shared__ uint4 img_[TW][4 * 64];
   __shared__ SlotRec rec_[TW][8];
