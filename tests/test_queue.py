@@ -108,6 +108,43 @@ def test_queue_seal_then_open_bit_exact():
 
 
 @pytest.mark.gpu
+def test_one_producer_uses_the_whole_ring():
+    """One producer thread submits 3,000 packets into a 4,096-slot queue before anything is reaped:
+    its own lane holds 64 slots (4096 / 64 lanes), so the other 2,936 come from other lanes'
+    free rings, 32 at a time through the lane's stash; every sealed packet is then compared with
+    the oracle, and the slots go back to their home lanes (a second round fits again)."""
+    W = wg()
+    eng = W.Engine(0, key_slots=4)
+    q = None
+    try:
+        keys = splitmix_np(2201, 32 * 4)
+        eng.set_keys(0, keys.tobytes())
+        q = eng.queue("seal", capacity=4096)
+        for rnd in range(2):
+            sent = {}
+            for i in range(3000):
+                L = (i * 37 + rnd) % 1500
+                pt = splitmix_bytes(rnd * 100000 + i, L)
+                sent[i] = (i % 4, (rnd << 32) | i, pt)
+                q.submit(i % 4, (rnd << 32) | i, pt, i)
+            got = {}
+            deadline = time.monotonic() + 30
+            while len(got) < 3000:
+                assert time.monotonic() < deadline, (len(got), q.stats())
+                for user, ctr, st, data in q.reap(4096, 100000):
+                    assert st == 0, st
+                    got[user] = (ctr, data)
+            for i, (slot, ctr, pt) in sent.items():
+                key = keys[32 * slot:32 * slot + 32].tobytes()
+                assert got[i][0] == ctr
+                assert got[i][1] == O.c_aead_seal(key, O.transport_nonce(ctr), pt), (rnd, i)
+    finally:
+        if q is not None:
+            q.close()
+        eng.close()
+
+
+@pytest.mark.gpu
 def test_queue_c_harness_transport_manager_shape():
     """tools/queue_bench: 16 producer threads submit 1420-B packets to a seal queue, a forwarder
     reaps them and submits each ct || tag to an open queue, a verifier checks every status and byte
