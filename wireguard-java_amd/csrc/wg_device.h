@@ -213,6 +213,13 @@ __device__ __forceinline__ void poly_r_limbs(uint32_t k0, uint32_t k1, uint32_t 
 // carries fit 32 bits) and the wrap carry from d4 is < 2^29.3 (so 5c < 2^32).
 // Each limb's carry seeds the next limb's v_mad_u64_u32 accumulator chain, so a
 // step costs 25 mads + 5 alignbits + 5 ands (+ the 2^130 wrap) and no 64-bit adds.
+// one v_mad_u64_u32 (d = a * b + c) as an asm statement: a chain of them keeps each limb's carry in
+// the accumulator instead of a separate 64-bit add
+__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
+  uint64_t d, cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(cc) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
 #ifdef WG_POLY_C  // the plain-C product (the compiler adds each limb's carry with a separate 64-bit add)
 __device__ __forceinline__ void poly_mul(uint32_t h[5], const uint32_t r[5], const uint32_t s[5]) {
   const uint32_t h0 = h[0], h1 = h[1], h2 = h[2], h3 = h[3], h4 = h[4];
@@ -241,11 +248,6 @@ __device__ __forceinline__ void poly_mul(uint32_t h[5], const uint32_t r[5], con
 // previous limb's carry instead of the compiler adding the carry to a separately formed
 // chain: -1.4% VALU instructions per k_transport launch (SQ_INSTS_VALU 37.70 M -> 37.18 M on
 // C1), bit-exact.
-__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
-  uint64_t d, cc;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(cc) : "v"(a), "v"(b), "v"(c));
-  return d;
-}
 __device__ __forceinline__ void poly_mul(uint32_t h[5], const uint32_t r[5], const uint32_t s[5]) {
   const uint32_t h0 = h[0], h1 = h[1], h2 = h[2], h3 = h[3], h4 = h[4];
   uint64_t d = mad64(h0, r[0], mad64(h1, s[4], mad64(h2, s[3], mad64(h3, s[2], (uint64_t)h4 * s[1]))));
@@ -264,6 +266,34 @@ __device__ __forceinline__ void poly_mul(uint32_t h[5], const uint32_t r[5], con
   h[1] += c;
 }
 #endif
+
+// Two Horner steps in one reduction: h = h * q + m * r (q = r^2; the caller adds the next
+// chunk), both products in one carry-seeded v_mad_u64_u32 chain per limb (tools/microbench20.hip
+// variant C: 239.9 cycles per chunk and wave against 281.9 for two poly_mul steps). Bounds: h < 2^27,
+// m < 2^26, q and r limbs < 2^26 + 2^8 => each limb sum < 2^60; limb 4 holds no 5x terms, so its
+// sum is < 2^56 and the wrap carry c < 2^30, whose 5c is added in 64 bits.
+__device__ __forceinline__ void poly_mul2(uint32_t h[5], const uint32_t q[5], const uint32_t qs[5], const uint32_t m[5],
+                                          const uint32_t r[5], const uint32_t s[5]) {
+  const uint32_t h0 = h[0], h1 = h[1], h2 = h[2], h3 = h[3], h4 = h[4];
+  uint64_t d = mad64(h0, q[0], mad64(h1, qs[4], mad64(h2, qs[3], mad64(h3, qs[2], (uint64_t)h4 * qs[1]))));
+  d = mad64(m[0], r[0], mad64(m[1], s[4], mad64(m[2], s[3], mad64(m[3], s[2], mad64(m[4], s[1], d)))));
+  h[0] = (uint32_t)d & M26;
+  d = mad64(h4, qs[2], mad64(h3, qs[3], mad64(h2, qs[4], mad64(h1, q[0], mad64(h0, q[1], d >> 26)))));
+  d = mad64(m[4], s[2], mad64(m[3], s[3], mad64(m[2], s[4], mad64(m[1], r[0], mad64(m[0], r[1], d)))));
+  h[1] = (uint32_t)d & M26;
+  d = mad64(h4, qs[3], mad64(h3, qs[4], mad64(h2, q[0], mad64(h1, q[1], mad64(h0, q[2], d >> 26)))));
+  d = mad64(m[4], s[3], mad64(m[3], s[4], mad64(m[2], r[0], mad64(m[1], r[1], mad64(m[0], r[2], d)))));
+  h[2] = (uint32_t)d & M26;
+  d = mad64(h4, qs[4], mad64(h3, q[0], mad64(h2, q[1], mad64(h1, q[2], mad64(h0, q[3], d >> 26)))));
+  d = mad64(m[4], s[4], mad64(m[3], r[0], mad64(m[2], r[1], mad64(m[1], r[2], mad64(m[0], r[3], d)))));
+  h[3] = (uint32_t)d & M26;
+  d = mad64(h4, q[0], mad64(h3, q[1], mad64(h2, q[2], mad64(h1, q[3], mad64(h0, q[4], d >> 26)))));
+  d = mad64(m[4], r[0], mad64(m[3], r[1], mad64(m[2], r[2], mad64(m[1], r[3], mad64(m[0], r[4], d)))));
+  h[4] = (uint32_t)d & M26;
+  const uint64_t t = (uint64_t)(uint32_t)(d >> 26) * 5u + h[0];
+  h[0] = (uint32_t)t & M26;
+  h[1] += (uint32_t)(t >> 26);
+}
 
 __device__ __forceinline__ void poly_scale5(const uint32_t r[5], uint32_t s[5]) {
   s[0] = 0;

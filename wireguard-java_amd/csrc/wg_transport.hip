@@ -563,9 +563,19 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
           acc[i] = 0;
         }
         if (j == 0) {
+#ifdef WG_HORNER2
+          // R and Q = R^2 (the two-chunk Horner step); their 5x forms are formed where used
+          uint32_t Q[5] = {R[0], R[1], R[2], R[3], R[4]}, Rs[5];
+          poly_scale5(R, Rs);
+          poly_mul(Q, R, Rs);
+          rec[s].R0 = make_uint4(R[0], R[1], R[2], R[3]);
+          rec[s].R1 = make_uint4(R[4], Q[0], Q[1], Q[2]);
+          rec[s].R2 = make_uint4(Q[3], Q[4], 0u, 0u);
+#else
           rec[s].R0 = make_uint4(R[0], R[1], R[2], R[3]);
           rec[s].R1 = make_uint4(R[4], 5u * R[1], 5u * R[2], 5u * R[3]);
           rec[s].R2 = make_uint4(5u * R[4], 0u, 0u, 0u);
+#endif
         }
       }
       wave_lds_sync();
@@ -590,6 +600,43 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         // chunk ci of the round sits in lane (ci >> 2) + 1 - G round of the slot, row ci & 3
         const uint4* ip = &img[64u * (c0 & 3u) + (lane & ~JM) + ((c0 + 4u) >> 2) - G * round];
         const uint4 q0 = rec[s].R0, q1 = rec[s].R1, q2 = rec[s].R2;
+#ifdef WG_HORNER2
+        // (opt-in, -DWG_HORNER2) two chunks per reduction where the round has them:
+        // acc = acc R^2 + m_t R + m_(t+1). Bit-exact, but it spills 2 VGPRs in k_step<8> and ran
+        // C1 1.2% slower (C2 equal) in an alternating A/B (profiles/r04_horner2_ab.txt)
+        const uint32_t R[5] = {q0.x, q0.y, q0.z, q0.w, q1.x};
+        const uint32_t Rs[5] = {0u, 5u * q0.y, 5u * q0.z, 5u * q0.w, 5u * q1.x};
+        const uint32_t Q[5] = {q1.y, q1.z, q1.w, q2.x, q2.y};
+        const uint32_t Qs[5] = {0u, 5u * q1.z, 5u * q1.w, 5u * q2.x, 5u * q2.y};
+        const uint32_t nst = c0 < c_end ? min(4u, (c_end - c0 + G - 1u) / G) : 0u;  // chunks this round
+#pragma unroll
+        for (uint32_t t = 0; t < 4u; t += 2u) {
+          if (t < nst) {
+            const uint4 v = ip[(G / 4u) * t];
+            uint32_t m0[5];
+            poly_block_limbs(v.x, v.y, v.z, v.w, 1u << 24, m0);
+            if (t + 1u < nst) {
+              if (round != 0 || t != 0) {
+                poly_mul2(acc, Q, Qs, m0, R, Rs);
+              } else {  // a packet's first two chunks: acc = m0 R (acc is still 0)
+#pragma unroll
+                for (int i = 0; i < 5; ++i) acc[i] = m0[i];
+                poly_mul(acc, R, Rs);
+              }
+              // the second chunk is read after the product (its limbs are not live across it)
+              const uint4 w = ip[(G / 4u) * (t + 1u)];
+              uint32_t m1[5];
+              poly_block_limbs(w.x, w.y, w.z, w.w, 1u << 24, m1);
+#pragma unroll
+              for (int i = 0; i < 5; ++i) acc[i] += m1[i];
+            } else {
+              if (round != 0 || t != 0) poly_mul(acc, R, Rs);
+#pragma unroll
+              for (int i = 0; i < 5; ++i) acc[i] += m0[i];
+            }
+          }
+        }
+#else
         const uint32_t R[5] = {q0.x, q0.y, q0.z, q0.w, q1.x};
         const uint32_t Rs[5] = {0u, q1.y, q1.z, q1.w, q2.x};
 #pragma unroll
@@ -608,6 +655,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
             for (int i = 0; i < 5; ++i) acc[i] += cl[i];
           }
         }
+#endif
       }
     }
 
@@ -621,9 +669,14 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         if (mac_pass) {
           if (valid) {
             if (j == JM && ((len + 15u) >> 4) >= 4u * G * round + 4u * G - 4u) {  // length block not taken in the loop
-              const uint4 q0 = rec[s].R0, q1 = rec[s].R1, q2 = rec[s].R2;
+              const uint4 q0 = rec[s].R0, q1 = rec[s].R1;
               const uint32_t R[5] = {q0.x, q0.y, q0.z, q0.w, q1.x};
+#ifdef WG_HORNER2
+              const uint32_t Rs[5] = {0u, 5u * q0.y, 5u * q0.z, 5u * q0.w, 5u * q1.x};
+#else
+              const uint4 q2 = rec[s].R2;
               const uint32_t Rs[5] = {0u, q1.y, q1.z, q1.w, q2.x};
+#endif
               poly_mul(acc, R, Rs);
               acc[2] += (len << 12) & M26;  // le64(len) at bit 64: limb 2 holds bits 52..77
               acc[3] += len >> 14;
