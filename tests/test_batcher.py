@@ -256,10 +256,9 @@ def test_held_caller_delays_nobody():
     assert j["failures"] == 0 and j["held_rc"] == 0
     assert j["held_us"] >= 50000
     assert j["lat_us"]["p999"] < 2000, j["lat_us"]
-    # the max, too, unless the box's CPU quota stalled the whole process meanwhile (17 busy threads
-    # on 16 CPUs of quota): then still far below the 50 ms a blocked wave would add
-    bound = 2000 if j["throttled_periods"] == 0 else 20000
-    assert j["lat_us"]["max"] < bound, (j["lat_us"], j["throttled_periods"])
+    # the single slowest of the 32,000 calls: 0.6-3.5 ms on the boxes so far (one outlier per run at
+    # most), far below the 50 ms that waiting for the held entry would add
+    assert j["lat_us"]["max"] < 20000, (j["lat_us"], j["throttled_periods"])
 
 
 @pytest.mark.gpu
