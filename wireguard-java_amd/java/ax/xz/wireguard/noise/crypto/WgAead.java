@@ -38,7 +38,7 @@ public final class WgAead {
 	static final MethodHandle SELFTEST, CTX_CREATE, LAST_ERROR, KEYS_SET, KEYS_ZERO, SEAL1, OPEN1, AEAD_HOST,
 		SEAL_BATCH, OPEN_BATCH, SYNC, SEAL_HOST, OPEN_HOST, HOST_ALLOC, HOST_FREE, FRAME_SEAL, PARSE_OPEN,
 		FILTER_SET, SLOT_FILTERS_SET, REPLAY_ENABLE, REPLAY_RESET, RX_CHECK, DUPLEX_BATCH, QUEUE_CREATE,
-		QUEUE_DESTROY, SUBMIT_SEAL, SUBMIT_OPEN, REAP, REAP_DONE;
+		QUEUE_DESTROY, SUBMIT_SEAL, SUBMIT_OPEN, REAP, REAP_DONE, NUMA_NODE;
 
 	/** The process-wide context (one HIP device, its stream and its device key table). */
 	static final MemorySegment CTX;
@@ -100,6 +100,8 @@ public final class WgAead {
 			JAVA_LONG, ADDRESS, JAVA_INT, JAVA_LONG));
 		REAP = down(linker, symbols, "wg_reap", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT, JAVA_INT));
 		REAP_DONE = down(linker, symbols, "wg_reap_done", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT));
+		// where to place the threads that feed the GPU (a queue's dispatcher already runs there)
+		NUMA_NODE = down(linker, symbols, "wg_device_numa_node", FunctionDescriptor.of(JAVA_INT, JAVA_INT));
 
 		int device = Integer.getInteger("wg.device", 0);
 		KEY_SLOTS = Integer.getInteger("wg.keySlots", 65536);
@@ -119,6 +121,19 @@ public final class WgAead {
 	}
 
 	private WgAead() {}
+
+	/**
+	 * NUMA node of the GPU (-1 if unknown): TransportManager's pools are best started on its CPUs
+	 * (numactl --cpunodebind, or a thread factory that sets the affinity), as the queue's
+	 * dispatcher thread is.
+	 */
+	public static int numaNode() {
+		try {
+			return (int) NUMA_NODE.invokeExact(Integer.getInteger("wg.device", 0));
+		} catch (Throwable e) {
+			throw new RuntimeException(e);
+		}
+	}
 
 	private static MethodHandle down(Linker linker, SymbolLookup symbols, String name, FunctionDescriptor fd) {
 		return symbols.find(name).map(addr -> linker.downcallHandle(addr, fd)).orElseThrow();
