@@ -49,7 +49,7 @@ constexpr uint32_t kRxNoFilter = 0xFFFFFFFFu;
 constexpr uint64_t kRejectAfter = ~0ull - 8191ull - 1ull;  // 2^64 - 2^13 - 1
 constexpr uint64_t kEmptyKey = ~0ull;                      // counters that large are rejected first
 constexpr uint32_t kTopWays = 8;         // copies of each slot's new top (spread same-address atomics)
-constexpr size_t kFlagBytes = 64 * (2 + kTopWays);  // order flag | done count | kTopWays group counts
+constexpr size_t kFlagBytes = 64 * (2 + kTopWays);  // order flags (2) | done count | kTopWays group counts
 // key slots the last block of k_rp_judge advances: one peer's 64K packets in order 25 us per
 // check against 31 as separate launches, but 1024 interleaved slots 65 against 60 (the last block
 // walks every slot), so larger tables launch the advance (profiles/r04_rx_launches.txt)
@@ -70,6 +70,7 @@ struct RxState {
   DevBuf d_pos;             // per packet: its (slot, counter) entry in d_tab, or ~0
   DevBuf d_flag;            // the order flag, k_rp_judge's finished blocks and groups, 64 B apart (0 between calls)
   bool five = false;        // WG_RX_LAUNCHES=5: decide and advance as two launches (A/B)
+  uint64_t checks = 0;      // replay checks queued: the order flag alternates between two words
   hipEvent_t ev = nullptr;  // last use of the replay scratch, and its stream (stream-ordered reuse)
   hipStream_t ev_stream = (hipStream_t)-1;
   DevBuf d_tables;          // wgt::RxTables for the fused open (WG_F_RX_FILTER)
@@ -209,6 +210,7 @@ struct RxParams {
   uint32_t tab_size;
   uint32_t* pos;
   uint32_t* unsorted;  // 0 while the batch's (slot, counter) pairs strictly increase with the index
+  uint32_t* unsorted_next;  // the next check's flag word (checks alternate between two words)
   uint32_t* done_blocks;  // k_rp_judge: blocks finished (0 between calls)
 };
 
@@ -557,7 +559,9 @@ __global__ void __launch_bounds__(256) k_rp_fixmark(RxParams P) {
   }
   rp_mark_at(P, i, false);
   if (own_entry) P.tab[P.pos[i]] = ~0u;
-  if (i == 0) *P.unsorted = 0u;  // every reader of the flag ran before this launch
+  // the next check's flag, not this one's: every thread of this launch reads this check's flag, and
+  // a block that starts after thread 0 has cleared it would skip its fix-ups
+  if (i == 0) *P.unsorted_next = 0u;
 }
 __global__ void __launch_bounds__(256) k_rp_mark(RxParams P) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
@@ -755,7 +759,9 @@ int wg_rx_check(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* pt, ui
     P.tab = (uint32_t*)r->d_tab.p;
     P.tab_size = r->tab_size;
     P.pos = (uint32_t*)r->d_pos.p;
-    P.unsorted = (uint32_t*)r->d_flag.p;
+    P.unsorted = (uint32_t*)r->d_flag.p + (r->checks & 1u);
+    P.unsorted_next = (uint32_t*)r->d_flag.p + ((r->checks + 1u) & 1u);
+    ++r->checks;
     P.done_blocks = (uint32_t*)r->d_flag.p + 16;  // its own line; group counters on the next lines
     if (!r->five) {
       const bool inl = c->key_slots <= kAdvanceInline;
