@@ -41,6 +41,7 @@ extern "C" {
 #define WG_E2BIG (-7)      /* packet longer than WG_MAX_PACKET */
 #define WG_EDEVICE (-5)    /* HIP runtime error (message via wg_last_error) */
 #define WG_ESELFTEST (-74) /* known-answer self test failed */
+#define WG_EAGAIN (-11)    /* wg_submit_*: no free queue slot within the queue's submit timeout */
 
 #define WG_PKT_OK 0u
 #define WG_PKT_BADTAG 1u
@@ -337,6 +338,10 @@ int wg_rx_check(wg_ctx* ctx, const wg_pkt* desc_dev, uint32_t n, const uint8_t* 
 int wg_seal1(wg_ctx* ctx, uint32_t key_slot, uint64_t counter, const uint8_t* pt, uint32_t len, uint8_t* out);
 int wg_open1(wg_ctx* ctx, uint32_t key_slot, uint64_t counter, const uint8_t* in, uint32_t len, uint8_t* pt);
 int wg_pp_config(wg_ctx* ctx, uint32_t waves, uint32_t idle_us);
+/* Diagnostic: the stages of the calling thread's last wg_seal1 / wg_open1, in ns (out[0..7]: total,
+ * claim, publish, wait for the completion, device service time, copy-out, slept on the futex 0/1,
+ * relaunched the server 0/1); tools/batcher_bench stamps=1 reports the slowest call's. */
+int wg_pp_last_call(uint64_t* out, uint32_t n);
 int wg_batcher_config(wg_ctx* ctx, uint32_t max_batch, uint32_t window_us);
 int wg_batcher_stats(wg_ctx* ctx, uint64_t* launches, uint64_t* packets);
 int wg_seal_host(wg_ctx* ctx, const wg_pkt* desc_host, uint32_t n, const uint8_t* in_host, uint64_t in_size,
@@ -356,8 +361,11 @@ int wg_open_host(wg_ctx* ctx, const wg_pkt* desc_host, uint32_t n, const uint8_t
  *     at most WG_QUEUE_MAX_LEN), batches of at most max_batch packets (0 = 8192).
  *   wg_submit_seal(q, key_slot, counter, pt, len, user): copies the plaintext into a free slot
  *     and queues it; the nonce is LE64(counter) || 0^4 (SymmetricKeypair.java:52-61), the key
- *     the device key table's key_slot. Blocks only while every slot is in use (until the consumer
- *     calls wg_reap_done). Thread-safe: any number of producers.
+ *     the one key_slot holds at the time of the submit (copied into the slot with the packet, as the
+ *     reference's synchronous cipher() uses the key it holds when called: a later wg_keys_set /
+ *     wg_keys_zero of the slot does not change a queued packet). Blocks only while every slot is in
+ *     use (until the consumer calls wg_reap_done), and then at most the queue's submit timeout:
+ *     returns WG_EAGAIN after it. Thread-safe: any number of producers.
  *   wg_submit_open(q, key_slot, counter, ct_tag, len, user): the same for ct || tag (len + 16 B).
  *   wg_reap(q, out, max, timeout_us): up to max completions (waits up to timeout_us for the
  *     first); returns how many, or a negative error. completion.data points into the queue's
@@ -366,6 +374,9 @@ int wg_open_host(wg_ctx* ctx, const wg_pkt* desc_host, uint32_t n, const uint8_t
  *     come back in batch order, not in submission order.
  *   wg_reap_done(q, c, n): the consumer is done with these completions (their slots are reused);
  *     each completion exactly once (a slot handed back twice would be given to two producers).
+ *   wg_queue_set_submit_timeout(q, timeout_us): how long wg_submit_* waits for a free slot before it
+ *     returns WG_EAGAIN (0, the default: without bound). A consumer that stalls then cannot wedge the
+ *     producers (ForkJoinPool workers) for good.
  *   wg_queue_destroy: waits for the batches in flight; unreaped completions are dropped. Call it
  *     only once no thread is inside (or can still enter) wg_submit_* / wg_reap* on this queue.
  * A producer thread keeps up to 32 slots taken from other lanes in its lane's stash; slots stashed
@@ -390,6 +401,7 @@ int wg_submit_open(wg_queue* q, uint32_t key_slot, uint64_t counter, const uint8
 int wg_reap(wg_queue* q, wg_completion* out, uint32_t max, uint32_t timeout_us);
 int wg_reap_done(wg_queue* q, const wg_completion* done, uint32_t n);
 int wg_queue_stats(wg_queue* q, uint64_t* batches, uint64_t* packets);
+int wg_queue_set_submit_timeout(wg_queue* q, uint32_t timeout_us);
 
 /* Pinned host rings for the host path (the reference's packet buffers come from
  * a native pool, Pool.java:96; pinning them makes wg_seal_host/wg_open_host zero-copy).

@@ -1,0 +1,90 @@
+"""The benchmark checks the kernel it times (pytest -m gpu).
+
+bench.py's headline step is two k_step launches, one per HIP stream, each sealing and then
+opening half of C1 (65,536 x 1,420 B, one key). Each half is 32,768 packets, so its grid is
+half the resident waves and the launch takes the k_step<8, 4> build (wg_capi.hip,
+launch_after_seal). These tests pin that exact shape against the oracle, and show that the
+bench line's own check (`verified`, `oracle_sample`) fails when k_step writes a wrong tag
+(test hook WG_TEST_STEP_FLIP).
+
+Reference: ChaCha20Poly1305.java:31-60 (poly1305AeadEncrypt / Decrypt), SymmetricKeypair.java:52-83
+(nonce = LE64(counter) || 0^4).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from wgtest import ROOT, oracle, splitmix_np, wg
+
+pytestmark = pytest.mark.gpu
+O = oracle()
+
+
+def test_bench_two_stream_step_every_packet_vs_oracle(engine):
+    """The bench's timed shape: two streams, each one WG_F_AFTER_SEAL k_step over 32,768 packets of
+    shared buffers; three steps in a row so launches of different steps overlap. Every ct || tag is
+    compared with the oracle, every plaintext with the input, every status must be OK."""
+    import torch
+    W = wg()
+    dev = torch.device("cuda", 0)
+    n, L, stride = 65536, 1420, 1440
+    keys = splitmix_np(0xC0FFEE, 32)
+    engine.set_keys(0, keys.tobytes())
+    off = np.arange(n, dtype=np.uint64) * stride
+    desc = W.pack_desc(off, off, np.arange(n, dtype=np.uint64), L, 0)
+    pt = splitmix_np(0x5EED, n * stride)
+    d_desc = torch.from_numpy(W.desc_as_int64(desc)).to(dev)
+    d_pt = torch.from_numpy(pt).to(dev)
+    d_ct = torch.full((n * stride,), 0x5A, dtype=torch.uint8, device=dev)
+    d_back = torch.full((n * stride,), 0xA5, dtype=torch.uint8, device=dev)
+    status = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    main = torch.cuda.current_stream()
+    side = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    cuts = [0, n // 2, n]
+    for s_ in side:
+        s_.wait_stream(main)
+    for _ in range(3):
+        for i, s_ in enumerate(side):
+            a, b = cuts[i], cuts[i + 1]
+            with torch.cuda.stream(s_):
+                engine.duplex(d_desc[a:b], d_pt, d_ct, L, d_desc[a:b], d_ct, d_back, status[a:b], L,
+                              uniform=True, after_seal=True)
+    for s_ in side:
+        main.wait_stream(s_)
+    torch.cuda.synchronize()
+    ref = np.zeros(n * stride, np.uint8)
+    O.seal_batch(desc, pt, ref, keys, threads=16)
+    ct = d_ct.cpu().numpy().reshape(n, stride)
+    ref = ref.reshape(n, stride)
+    bad = np.nonzero(~np.all(ct[:, :L + 16] == ref[:, :L + 16], axis=1))[0]
+    assert bad.size == 0, f"{bad.size} packets' ct||tag differ from the oracle (first {bad[:8]})"
+    assert not status.cpu().numpy().any()
+    back = d_back.cpu().numpy().reshape(n, stride)
+    assert np.array_equal(back[:, :L], pt.reshape(n, stride)[:, :L])
+
+
+def _bench(extra_env):
+    env = dict(os.environ, **extra_env)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--ramp-ms", "0"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert lines, f"no JSON line (rc {p.returncode}): {p.stderr[-2000:]}"
+    return p.returncode, json.loads(lines[-1])
+
+
+def test_bench_line_fails_when_k_step_writes_a_wrong_tag():
+    """WG_TEST_STEP_FLIP=64: k_step flips one tag bit of every 64th packet between its seal and open
+    halves. The bench line must then report verified false and oracle_sample.bit_exact false, and the
+    bench must exit 3. Without the hook the same short run is verified and bit-exact."""
+    rc, line = _bench({"WG_TEST_STEP_FLIP": "64"})
+    assert rc == 3, line
+    assert line["verified"] is False
+    assert line["oracle_sample"]["bit_exact"] is False
+    rc, line = _bench({})
+    assert rc == 0, line
+    assert line["verified"] is True and line["oracle_sample"]["bit_exact"] is True
+    assert line["config"]["streams"] == 2 and line["roofline"]["kernel_names"] == ["k_step"]

@@ -403,3 +403,60 @@ def test_rx_argument_contract(engine):
     assert lib.wg_rx_check(engine.ctx, d.data_ptr(), 0, None, 0, None, 3, None) == 0  # n = 0
     assert lib.wg_slot_filters_set(engine.ctx, engine.key_slots, 1, None) == E  # NULL ids with n > 0
     assert lib.wg_filter_set(engine.ctx, W._lib.WG_MAX_FILTERS, None, 0) == W._lib.WG_ERANGE
+
+
+@pytest.mark.parametrize("mutant", [False, True])
+def test_replay_flag_protocol_under_block_skew(mutant):
+    """Regression test of the order-flag race fixed in round 4 (98a2832): k_rp_fixmark cleared the
+    order flag that its own later-starting blocks still read, so they skipped their duplicate
+    fix-ups and a repeated (slot, counter) could be accepted twice. WG_RX_TEST_SKEW delays every
+    block but block 0 of each replay launch by 30 us, so block 0 always finishes first.
+    Consecutive duplicate-laden checks must then still match the oracle (flag words, done counts,
+    group counts and new-top copies all read after the skew). WG_RX_TEST_MUTANT=1 puts the old flag
+    clearing back: the same checks must then disagree with the oracle, which shows that the skew
+    exposes the race. Reference: TransportManager.java:98-119 (the window itself is unpinned)."""
+    import os
+    torch, dev = _dev()
+    W = wg()
+    env = {"WG_RX_LAUNCHES": "3", "WG_RX_TEST_SKEW": "30", "WG_RX_TEST_MUTANT": "1" if mutant else "0"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        engine = W.Engine(0, key_slots=512)
+        engine.replay_enable(256)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    try:
+        engine.set_keys(0, splitmix_np(9, 32 * 16).tobytes())
+        o = rx.ReplayWindow(256)
+        rng = np.random.default_rng(77)
+        base = np.zeros(16, np.int64)
+        agree = []
+        for b in range(4):
+            n = 20000  # 79 blocks
+            slots = rng.integers(0, 16, n)
+            c64 = base[slots] + rng.integers(0, 300, n)
+            dup = rng.random(n) < 0.08
+            c64[dup] = np.maximum(c64[dup] - rng.integers(0, 200, dup.sum()), 0)
+            np.maximum.at(base, slots, c64)
+            ctr = c64.astype(np.uint64)
+            status = np.zeros(n, np.int64)
+            got = _run(engine, torch, dev, W, slots, ctr, [b""] * n, status, W._lib.WG_RX_REPLAY)
+            want = o.check_batch(slots, [int(x) for x in ctr], status)
+            same = got == want
+            for s_ in range(16):
+                top, words = engine.replay_state(s_, 256)
+                otop, owords = o.bitmap(s_)
+                same = same and top == otop and [int(x) for x in words] == owords
+            agree.append(same)
+            if not mutant:
+                assert same, b
+                assert any(x == rx.PKT_REPLAY for x in want)
+        if mutant:
+            assert not all(agree), "the skew did not expose the round-4 flag race"
+    finally:
+        engine.close()

@@ -159,6 +159,171 @@ def test_queue_c_harness_transport_manager_shape():
         assert j["bad"] == 0 and j["packets"] == int(args[0]) * int(args[1])
 
 
+def _with_env(env, fn):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+def _reap_all(q, n, timeout_s=30):
+    got = {}
+    deadline = time.monotonic() + timeout_s
+    while len(got) < n:
+        assert time.monotonic() < deadline, (len(got), q.stats())
+        for user, ctr, st, data in q.reap(4096, 100000):
+            got[user] = (ctr, st, data)
+    return got
+
+
+@pytest.mark.gpu
+def test_queued_packets_keep_the_key_they_were_submitted_with():
+    """A packet queued before wg_keys_zero / wg_keys_set of its key slot is sealed with the key the
+    slot held at the submit, never the zero key or the next keypair's (the kernel used to
+    read the device key table when the batch launched, so clean() between submit and launch sealed
+    packets under an all-zero key). The batching window is stretched to 300 ms (WG_QUEUE_WINDOW_US)
+    so every packet is still queued when the key changes. Reference: SymmetricKeypair.java:63-74, 85-93."""
+    W = wg()
+    eng = W.Engine(0, key_slots=4)
+    q = None
+    try:
+        k_old, k_new = splitmix_bytes(2301, 32), splitmix_bytes(2302, 32)
+        eng.set_keys(1, k_old)
+        q = _with_env({"WG_QUEUE_WINDOW_US": "300000", "WG_QUEUE_MIN_BATCH": "100000"},
+                      lambda: eng.queue("seal", capacity=1024))
+        pts = {i: splitmix_bytes(2400 + i, 100 + 13 * i) for i in range(40)}
+        for i in range(20):
+            q.submit(1, i, pts[i], i)
+        eng.zero_keys(1, 1)  # clean(): the queued packets keep k_old
+        for i in range(20, 30):
+            q.submit(1, i, pts[i], i)  # submitted after the zeroing: the zero key, as wg_seal1 would
+        eng.set_keys(1, k_new)
+        for i in range(30, 40):
+            q.submit(1, i, pts[i], i)
+        got = _reap_all(q, 40)
+        for i in range(40):
+            key = k_old if i < 20 else bytes(32) if i < 30 else k_new
+            ctr, st, data = got[i]
+            assert st == 0 and ctr == i
+            assert data == O.c_aead_seal(key, O.transport_nonce(i), pts[i]), i
+    finally:
+        if q is not None:
+            q.close()
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_submit_timeout_returns_eagain_when_nobody_reaps():
+    """wg_queue_set_submit_timeout: with every slot of a 64-slot queue sealed but not reaped, the next
+    submit returns WG_EAGAIN after the timeout instead of waiting for ever (the round-4 hang was a
+    caller that submitted more packets than the ring holds before reaping any); after the consumer
+    reaps, submits succeed again."""
+    W = wg()
+    eng = W.Engine(0, key_slots=1)
+    q = None
+    try:
+        eng.set_keys(0, splitmix_bytes(2501, 32))
+        q = eng.queue("seal", capacity=64)
+        q.set_submit_timeout(5000)
+        for i in range(64):
+            q.submit(0, i, b"x" * 64, i)
+        t0 = time.monotonic()
+        with pytest.raises(W.WgError) as ei:
+            q.submit(0, 64, b"x" * 64, 64)
+        assert ei.value.code == W._lib.WG_EAGAIN
+        assert time.monotonic() - t0 < 2.0
+        got = _reap_all(q, 64)
+        assert all(st == 0 for _, st, _ in got.values())
+        q.submit(0, 65, b"y" * 64, 65)
+        assert _reap_all(q, 1)[65][1] == 0
+    finally:
+        if q is not None:
+            q.close()
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_queue_beside_batch_calls_with_timing_and_another_kernel():
+    """A queue runs while another thread makes wg_seal_batch calls with timing on and the k_tile
+    kernel selected (the dispatcher launched without c->mu through whatever kernel the
+    context selected, racing the shared plan workspace and the timing-event list). The queue's
+    launches are now the transport kernel with their own keys and no timing events: both paths stay
+    bit-exact, and the timing list holds exactly the batch calls' launches."""
+    import torch
+    W = wg()
+    eng = W.Engine(0, key_slots=8)
+    q = None
+    try:
+        keys = splitmix_np(2601, 32 * 8)
+        eng.set_keys(0, keys.tobytes())
+        eng.set_kernel("tile")
+        q = eng.queue("seal", capacity=4096)
+        errors, sent = [], {}
+
+        def producer():
+            try:
+                for i in range(6000):
+                    pt = splitmix_bytes(2700 + i, (i * 53) % 1500)
+                    sent[i] = (i % 8, pt)
+                    q.submit(i % 8, i, pt, i)
+            except Exception as e:  # pragma: no cover - reported below
+                errors.append(repr(e))
+
+        got = {}
+
+        def consumer():
+            try:
+                deadline = time.monotonic() + 60
+                while len(got) < 6000 and time.monotonic() < deadline:
+                    for user, ctr, st, data in q.reap(4096, 20000):
+                        got[user] = (st, data)
+            except Exception as e:  # pragma: no cover
+                errors.append(repr(e))
+
+        th = [threading.Thread(target=producer, daemon=True), threading.Thread(target=consumer, daemon=True)]
+        for t in th:
+            t.start()
+        dev = torch.device("cuda", 0)
+        n, L = 2048, 700
+        off = np.arange(n, dtype=np.uint64) * 720
+        desc = W.pack_desc(off, off, np.arange(n, dtype=np.uint64), L, np.arange(n) % 8)
+        pt = splitmix_np(2801, n * 720)
+        ref = np.zeros_like(pt)
+        O.seal_batch(desc, pt, ref, keys, threads=8)
+        d_desc = torch.from_numpy(W.desc_as_int64(desc)).to(dev)
+        d_pt = torch.from_numpy(pt).to(dev)
+        eng.timing(True)
+        eng.timing_read()
+        calls = 0
+        while th[0].is_alive() and calls < 400:
+            d_ct = torch.zeros_like(d_pt)
+            eng.seal(d_desc, d_pt, d_ct, L)
+            torch.cuda.synchronize()
+            ct = d_ct.cpu().numpy().reshape(n, 720)
+            assert np.array_equal(ct[:, :L + 16], ref.reshape(n, 720)[:, :L + 16])
+            calls += 1
+        for t in th:
+            t.join(timeout=60)
+        _, launches = eng.timing_read()
+        eng.timing(False)
+        assert not errors, errors[:3]
+        assert launches == calls, (launches, calls)  # k_tile's mixed plan: one timed launch per call
+        assert len(got) == 6000
+        for i, (slot, p) in sent.items():
+            key = keys[32 * slot:32 * slot + 32].tobytes()
+            assert got[i][0] == 0 and got[i][1] == O.c_aead_seal(key, O.transport_nonce(i), p), i
+    finally:
+        if q is not None:
+            q.close()
+        eng.close()
+
+
 def test_queue_argument_contract():
     W = wg()
     lib = W.lib()
@@ -171,4 +336,5 @@ def test_queue_argument_contract():
     assert lib.wg_reap(None, None, 0, 0) == E
     assert lib.wg_reap_done(None, None, 0) == E
     assert lib.wg_queue_stats(None, None, None) == E
+    assert lib.wg_queue_set_submit_timeout(None, 0) == E
     assert lib.wg_queue_destroy(None) == 0

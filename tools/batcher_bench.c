@@ -14,8 +14,14 @@
  *   fail_launches=F the first F server launches are refused (WG_PP_TEST_FAIL_LAUNCHES); the warm-up
  *                   call must fail, every timed call must then succeed
  *   waves=W idle_us=I  wg_pp_config before the first call
+ *   stamps=1        after every call read its stages (wg_pp_last_call) and the thread's context
+ *                   switches (getrusage RUSAGE_THREAD): the slowest call's breakdown goes into the
+ *                   line ("slowest"), with the count of calls over 1 ms and how many of those were
+ *                   preempted (an involuntary context switch during the call)
  * Output: one JSON line. */
+#define _GNU_SOURCE
 #include <pthread.h>
+#include <sys/resource.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -33,6 +39,15 @@ static int g_gap_us;
 #define HOLD_COUNTER 0x0D0D0D0D0D0Dull
 static double g_held_us = -1.0;
 static int g_held_rc = 0;
+static int g_stamps;
+typedef struct {
+  double lat_us;
+  uint64_t st[8];   /* wg_pp_last_call */
+  long nivcsw, nvcsw; /* context switches of the thread during the call */
+  int op, thread;
+} slow_t;
+static slow_t* g_slowest;        /* per thread */
+static int* g_over1ms, *g_over1ms_preempted;
 
 static double now_us(void) {
   struct timespec t;
@@ -56,6 +71,8 @@ static void* worker(void* arg) {
   uint64_t ctr = (uint64_t)t << 40;
   uint32_t L = 0;
   for (int i = 0; i < g_calls; ++i) {
+    struct rusage ru0, ru1;
+    if (g_stamps) getrusage(RUSAGE_THREAD, &ru0);
     double t0 = now_us();
     int rc;
     if ((i & 1) == 0) {
@@ -66,7 +83,26 @@ static void* worker(void* arg) {
       if (rc == 0 && memcmp(back, pt, L) != 0) rc = -100;
       ++ctr;
     }
-    g_lat[(size_t)t * g_calls + i] = now_us() - t0;
+    const double lat = now_us() - t0;
+    g_lat[(size_t)t * g_calls + i] = lat;
+    if (g_stamps) {
+      uint64_t st[8];
+      wg_pp_last_call(st, 8);
+      getrusage(RUSAGE_THREAD, &ru1);
+      const long niv = ru1.ru_nivcsw - ru0.ru_nivcsw, nv = ru1.ru_nvcsw - ru0.ru_nvcsw;
+      if (lat > 1000.0) {
+        ++g_over1ms[t];
+        if (niv > 0) ++g_over1ms_preempted[t];
+      }
+      if (lat > g_slowest[t].lat_us) {
+        g_slowest[t].lat_us = lat;
+        memcpy(g_slowest[t].st, st, sizeof st);
+        g_slowest[t].nivcsw = niv;
+        g_slowest[t].nvcsw = nv;
+        g_slowest[t].op = i & 1;
+        g_slowest[t].thread = t;
+      }
+    }
     if (rc != 0) ++g_fail[t];
     g_bytes[t] += L;
     if (g_gap_us) {
@@ -121,6 +157,7 @@ int main(int argc, char** argv) {
     else if (!strncmp(argv[a], "fail_launches=", 14)) fail_launches = x;
     else if (!strncmp(argv[a], "waves=", 6)) waves = x;
     else if (!strncmp(argv[a], "idle_us=", 8)) idle_us = x;
+    else if (!strncmp(argv[a], "stamps=", 7)) g_stamps = x;
   }
   if (T < 1 || T > 1024 || g_calls < 2 || g_len < 0 || g_len > 1500) {
     fprintf(stderr, "usage: batcher_bench [threads] [calls] [len 0..1500] [gap_us= hold_us= fail_launches= waves= idle_us=]\n");
@@ -152,6 +189,9 @@ int main(int argc, char** argv) {
   g_lat = calloc((size_t)T * g_calls, sizeof(double));
   g_bytes = calloc(T, sizeof(uint64_t));
   g_fail = calloc(T, sizeof(int));
+  g_slowest = calloc(T, sizeof(slow_t));
+  g_over1ms = calloc(T, sizeof(int));
+  g_over1ms_preempted = calloc(T, sizeof(int));
   pthread_t th[1024];
   if (wg_pp_config(g_ctx, (uint32_t)waves, (uint32_t)idle_us) != WG_OK) {
     fprintf(stderr, "wg_pp_config: %s\n", wg_last_error());
@@ -185,16 +225,34 @@ int main(int argc, char** argv) {
     bytes += g_bytes[t];
     fails += g_fail[t];
   }
+  char slow[768] = "";
+  if (g_stamps) {
+    int w = 0, o1 = 0, o1p = 0;
+    for (int t = 0; t < T; ++t) {
+      if (g_slowest[t].lat_us > g_slowest[w].lat_us) w = t;
+      o1 += g_over1ms[t];
+      o1p += g_over1ms_preempted[t];
+    }
+    const slow_t* x = &g_slowest[w];
+    snprintf(slow, sizeof slow,
+             ", \"slowest\": {\"lat_us\": %.1f, \"op\": \"%s\", \"thread\": %d, \"claim_us\": %.1f, "
+             "\"publish_us\": %.1f, \"wait_us\": %.1f, \"device_service_us\": %.1f, \"copy_out_us\": %.1f, "
+             "\"slept\": %llu, \"relaunched\": %llu, \"involuntary_csw\": %ld, \"voluntary_csw\": %ld}, "
+             "\"calls_over_1ms\": %d, \"calls_over_1ms_preempted\": %d",
+             x->lat_us, x->op ? "open" : "seal", x->thread, x->st[1] * 1e-3, x->st[2] * 1e-3, x->st[3] * 1e-3,
+             x->st[4] * 1e-3, x->st[5] * 1e-3, (unsigned long long)x->st[6], (unsigned long long)x->st[7],
+             x->nivcsw, x->nvcsw, o1, o1p);
+  }
   printf("{\"tool\": \"batcher_bench\", \"threads\": %d, \"calls_per_thread\": %d, \"len\": \"%s\", "
          "\"calls\": %zu, \"failures\": %d, \"wall_s\": %.4f, \"calls_per_s\": %.0f, "
          "\"payload_gib_s\": %.4f, \"lat_us\": {\"p50\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"p999\": %.1f, "
          "\"max\": %.1f}, \"launches\": %llu, \"mean_batch\": %.1f, \"gap_us\": %d, \"waves\": %d, "
-         "\"fail_launches\": %d, \"hold_us\": %d, \"held_us\": %.1f, \"held_rc\": %d, \"throttled_periods\": %llu}\n",
+         "\"fail_launches\": %d, \"hold_us\": %d, \"held_us\": %.1f, \"held_rc\": %d, \"throttled_periods\": %llu%s}\n",
          T, g_calls, g_len ? argv[3] : "mixed 64..1500", n, fails, wall * 1e-6, n / (wall * 1e-6),
          bytes / (wall * 1e-6) / (double)(1u << 30), g_lat[n / 2], g_lat[n * 9 / 10], g_lat[n * 99 / 100],
          g_lat[n * 999 / 1000], g_lat[n - 1], (unsigned long long)(l1 - l0),
          (l1 > l0) ? (double)(p1 - p0) / (double)(l1 - l0) : 0.0, g_gap_us, waves, fail_launches, hold_us,
-         g_held_us, g_held_rc, thr1 - thr0);
+         g_held_us, g_held_rc, thr1 - thr0, slow);
   wg_ctx_destroy(g_ctx);
   return (fails || g_held_rc) ? 1 : 0;
 }

@@ -20,6 +20,7 @@ WG_ERANGE = -34
 WG_E2BIG = -7
 WG_EDEVICE = -5
 WG_ESELFTEST = -74
+WG_EAGAIN = -11
 WG_PKT_OK = 0
 WG_PKT_BADTAG = 1
 WG_PKT_BADHDR = 2
@@ -45,7 +46,7 @@ WG_F_RX_FILTER = 8
 WG_MODE_SEAL, WG_MODE_OPEN, WG_MODE_CIPHER, WG_MODE_MAC = 0, 1, 2, 3
 
 _ERRNAMES = {WG_EINVAL: "EINVAL", WG_ENOMEM: "ENOMEM", WG_ERANGE: "ERANGE", WG_E2BIG: "E2BIG",
-             WG_EDEVICE: "EDEVICE", WG_ESELFTEST: "ESELFTEST"}
+             WG_EDEVICE: "EDEVICE", WG_ESELFTEST: "ESELFTEST", WG_EAGAIN: "EAGAIN"}
 
 
 class WgError(RuntimeError):
@@ -122,6 +123,7 @@ SIGNATURES = [
     ("wg_seal1", _I, [_VP, _U32, _U64, _VP, _U32, _VP]),
     ("wg_open1", _I, [_VP, _U32, _U64, _VP, _U32, _VP]),
     ("wg_pp_config", _I, [_VP, _U32, _U32]),
+    ("wg_pp_last_call", _I, [ctypes.POINTER(_U64), _U32]),
     ("wg_batcher_config", _I, [_VP, _U32, _U32]),
     ("wg_batcher_stats", _I, [_VP, ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
     ("wg_queue_create", _I, [_VP, _I, _U32, _U32, _U32, ctypes.POINTER(_VP)]),
@@ -131,6 +133,7 @@ SIGNATURES = [
     ("wg_reap", _I, [_VP, ctypes.POINTER(WgCompletion), _U32, _U32]),
     ("wg_reap_done", _I, [_VP, ctypes.POINTER(WgCompletion), _U32]),
     ("wg_queue_stats", _I, [_VP, ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
+    ("wg_queue_set_submit_timeout", _I, [_VP, _U32]),
     ("wg_seal_host", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _U32, _U32]),
     ("wg_open_host", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _VP, _U32, _U32]),
     ("wg_host_alloc", _I, [_VP, _U64, ctypes.POINTER(_VP)]),

@@ -112,6 +112,9 @@ struct wg_ctx {
   // half-occupancy k_step grids (C2's longest-first pairs) take the build allocated for 4 waves per
   // SIMD: no SGPR spills, C2 +0.7% in 3 alternations (profiles/r04_wpe_ab.txt); WG_STEP_WPE4=0: not
   bool step_wpe4 = true;
+  // test hook WG_TEST_STEP_FLIP=N (power of two): the k_step launch's seal half writes a wrong tag for every
+  // packet whose index is a multiple of N (tests/test_gpu_bench.py: the bench must report verified false)
+  uint32_t test_flip = 0;
   // plan workspace: k_tile block scan, k_transport longest-first order
   DevBuf plan_nb, plan_prefix, plan_tiles, plan_ntiles, plan_tmp, lpt_hist, lpt_order;
   DevBuf lpt_hist2, lpt_order2;  // the open half of a wg_duplex_batch
@@ -123,7 +126,12 @@ struct wg_ctx {
   std::mutex mu;  // serialises host-API calls and plan workspace reuse
   PPServer* pp = nullptr;  // persistent per-packet server (wg_seal1 / wg_open1)
   std::mutex pp_mu;
-  std::vector<uint8_t> keys_host;  // host mirror of the key table: the per-packet path sends keys with the packet
+  // Host mirror of the key table, read by the paths that send a key WITH the packet (the per-packet
+  // server, the asynchronous queue): 4 words per slot behind a per-slot sequence lock, so readers
+  // (every submit) take no lock and share no written cache line; writers (wg_keys_set / wg_keys_zero)
+  // serialise on keys_mu. key_snapshot() reads a consistent key.
+  std::unique_ptr<std::atomic<uint64_t>[]> key_words;
+  std::unique_ptr<std::atomic<uint32_t>[]> key_seq;  // even: stable, odd: being written
   std::mutex keys_mu;
   RxState* rx = nullptr;  // receive-side checks (wg_rx.hip)
   // timing
@@ -145,6 +153,41 @@ struct DeviceGuard {
     if (prev >= 0) (void)hipSetDevice(prev);
   }
 };
+
+// The key of `slot` as the host mirror holds it now (sequence-lock read: retried while a writer is
+// inside wg_keys_set / wg_keys_zero for that slot, so the 32 bytes are never a mix of two keys).
+void key_snapshot(const wg_ctx* c, uint32_t slot, uint32_t key[8]) {
+  std::atomic<uint32_t>& sq = c->key_seq[slot];
+  for (;;) {
+    const uint32_t s1 = sq.load(std::memory_order_acquire);
+    if (s1 & 1u) {
+      __builtin_ia32_pause();
+      continue;
+    }
+    uint64_t w[4];
+    for (int i = 0; i < 4; ++i) w[i] = c->key_words[4u * slot + i].load(std::memory_order_relaxed);
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (sq.load(std::memory_order_relaxed) == s1) {
+      memcpy(key, w, 32);
+      return;
+    }
+  }
+}
+
+// Writes slots [first, first + n) of the host mirror (keys: n x 32 B, or NULL for zeros). Caller holds
+// c->keys_mu.
+void key_mirror_write(wg_ctx* c, uint32_t first, uint32_t n, const uint8_t* keys) {
+  for (uint32_t k = 0; k < n; ++k) {
+    std::atomic<uint32_t>& sq = c->key_seq[first + k];
+    const uint32_t s0 = sq.load(std::memory_order_relaxed);
+    sq.store(s0 + 1u, std::memory_order_relaxed);  // odd: readers retry
+    std::atomic_thread_fence(std::memory_order_release);
+    uint64_t w[4] = {0, 0, 0, 0};
+    if (keys) memcpy(w, keys + 32ull * k, 32);
+    for (int i = 0; i < 4; ++i) c->key_words[4ull * (first + k) + i].store(w[i], std::memory_order_relaxed);
+    sq.store(s0 + 2u, std::memory_order_release);
+  }
+}
 
 template <int MODE>
 uint32_t host_pkt_blocks(uint32_t len) {
@@ -420,11 +463,19 @@ SlotPlan slot_plan(const wg_ctx* c, uint32_t flags, uint32_t n) {
 // Transport seal/open through k_transport: persistent slots, 64 / G per wave. Each slot takes
 // ceil(n / resident slots) packets; mixed-length batches are ordered longest-first on
 // the device first (k_lpt_*), so the slots' snake over the order balances their rounds.
+// A launch that brings its own key table (the asynchronous queue: one key per ring slot, copied at
+// submit time) runs the transport kernel whatever kernel the context selects, touches no state shared
+// with the context's other callers (no plan workspace, no timing events) and so needs no c->mu.
+struct OwnKeys {
+  const uint32_t* keys;  // device-readable table, 8 words per entry
+  uint32_t slots;
+};
+
 template <int MODE>
 int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in, uint64_t in_size, uint8_t* out,
                      uint64_t out_size, uint32_t* status, uint32_t max_len, uint32_t flags, hipStream_t s,
                      const wgt::RxTables* rx = nullptr, DevBuf* own_hist = nullptr, DevBuf* own_order = nullptr,
-                     bool reuse_order = false) {
+                     bool reuse_order = false, const OwnKeys* own_keys = nullptr) {
   if (n == 0) return WG_OK;
   if (!desc || (((uintptr_t)desc) & 15u)) return fail(WG_EINVAL, "descriptor array must be non-NULL and 16-byte aligned");
   if (!in || !out) return fail(WG_EINVAL, "NULL buffer");
@@ -432,7 +483,7 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
   // an open whose buffers overlap runs the transport kernel whatever kernel is selected: only its
   // verify-first variant leaves a forged in-place packet's bytes untouched (ChaCha20Poly1305.java:40-56),
   // and every selectable kernel must write identical bytes (include/wgaead.h)
-  int kern = c->kern;
+  int kern = own_keys ? (int)KERN_TRANSPORT : c->kern;
   if (MODE == WG_MODE_OPEN && kern != KERN_TRANSPORT && open_overlaps(in, in_size, out, out_size)) kern = KERN_TRANSPORT;
   if (rx && kern != KERN_TRANSPORT) return fail(WG_EINVAL, "WG_F_RX_FILTER needs the transport kernel");
   // k_tile's uniform plan sizes every tile for max_len-long packets; WG_F_UNIFORM is only a
@@ -472,8 +523,13 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
                                 own ? *own_hist : c->lpt_hist, own ? *own_order : c->lpt_order, &P, &grid, &ordered,
                                 rx, own, reuse_order, sp.split);
   if (rc != WG_OK) return rc;
-  hipEvent_t ev;
-  record_start(c, s, &ev);
+  if (own_keys) {
+    if (!(flags & WG_F_UNIFORM) && !own) return fail(WG_EINVAL, "own-key launches plan without the shared workspace");
+    P.keys = own_keys->keys;
+    P.key_slots = own_keys->slots;
+  }
+  hipEvent_t ev = nullptr;
+  if (!own_keys) record_start(c, s, &ev);
   if constexpr (MODE == WG_MODE_OPEN) {
     if (open_overlaps(in, in_size, out, out_size)) {  // in-place opens verify first (k_transport<OPEN, G, true>)
       if (P.n_long) hipLaunchKernelGGL((wgt::k_transport_mixed<MODE, true>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
@@ -538,6 +594,7 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
                                         c->lpt_order, &PO, &go, &oo, nullptr, true, true, sp.split);
     // one issue-priority schedule over the seal and open halves (the rounds of both)
     if (PS.prio_step) PS.prio_step = PO.prio_step = 2u * PS.prio_step;
+    PS.test_flip = c->test_flip;
     if (rc == WG_OK && (gs != go || PS.slots != PO.slots || PS.order != PO.order))
       rc = fail(WG_EINVAL, "k_step: seal and open plans differ (%u / %u workgroups)", gs, go);
 #ifdef WG_DIAG
@@ -640,7 +697,8 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
     wg_ctx_destroy(c);
     return fail(WG_ENOMEM, "context allocation failed on device %d", device);
   }
-  c->keys_host.assign((size_t)key_slots * 32, 0);
+  c->key_words.reset(new std::atomic<uint64_t>[(size_t)key_slots * 4]());
+  c->key_seq.reset(new std::atomic<uint32_t>[key_slots]());
   for (int w = 0; w < 2; ++w)
     for (int k = 0; k < 3; ++k)
       c->resident_waves[w][k] = (uint32_t)std::max(bl[w][k], 1) * wgt::TW * (uint32_t)prop.multiProcessorCount;
@@ -654,6 +712,10 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   if (const char* e = getenv("WG_UNIFORM16")) c->uniform16 = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_PRIO")) c->prio_mode = atoi(e);
   if (const char* e = getenv("WG_STEP_WPE4")) c->step_wpe4 = atoi(e) != 0;
+  if (const char* e = getenv("WG_TEST_STEP_FLIP")) {
+    const long v = atol(e);
+    c->test_flip = (v > 0 && (v & (v - 1)) == 0) ? (uint32_t)v : 0u;
+  }
   *out = c;
   return WG_OK;
 }
@@ -661,7 +723,10 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
 int wg_ctx_destroy(wg_ctx* c) {
   if (!c) return WG_OK;
   pp_stop(c);
-  std::fill(c->keys_host.begin(), c->keys_host.end(), (uint8_t)0);
+  if (c->key_words) {
+    std::lock_guard<std::mutex> lk(c->keys_mu);
+    key_mirror_write(c, 0, c->key_slots, nullptr);
+  }
   DeviceGuard g(c->device);
   rx_free(c);
   if (c->keys) {
@@ -707,7 +772,7 @@ int wg_keys_set(wg_ctx* c, uint32_t first, uint32_t n, const uint8_t* keys_host)
   HIPTRY(hipMemcpyAsync((uint8_t*)c->keys + (size_t)first * 32, keys_host, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
   {
     std::lock_guard<std::mutex> lk2(c->keys_mu);
-    memcpy(c->keys_host.data() + (size_t)first * 32, keys_host, (size_t)n * 32);
+    key_mirror_write(c, first, n, keys_host);
   }
   int rc;
   if ((rc = rx_reset_slots(c, first, n, c->stream)) != WG_OK) return rc;  // new key: new session
@@ -724,7 +789,7 @@ int wg_keys_zero(wg_ctx* c, uint32_t first, uint32_t n) {
   HIPTRY(hipMemsetAsync((uint8_t*)c->keys + (size_t)first * 32, 0, (size_t)n * 32, c->stream));
   {
     std::lock_guard<std::mutex> lk2(c->keys_mu);
-    memset(c->keys_host.data() + (size_t)first * 32, 0, (size_t)n * 32);
+    key_mirror_write(c, first, n, nullptr);
   }
   int rc;
   if ((rc = rx_reset_slots(c, first, n, c->stream)) != WG_OK) return rc;

@@ -75,6 +75,8 @@ struct PPParams {
   uint32_t* exited;       // device memory: waves exited in this launch (zeroed before it)
   uint32_t* quit;         // device memory: raised by the first wave that decides the server leaves (zeroed)
   uint64_t* last;         // device memory: s_memrealtime of the last service in this launch (zeroed)
+  uint64_t* svc;          // device alias (pinned): per entry, s_memrealtime ticks from the wave seeing its
+                          // doorbell bit to its completion store (wg_pp_last_call's device service time)
   uint32_t waves;         // W (power of two, 1..64): wave w owns entries [w E, (w + 1) E), E = kRing / W
   uint32_t gen;
   uint64_t idle_ticks;    // s_memrealtime ticks (100 MHz)
@@ -107,7 +109,7 @@ constexpr uint32_t kFirstDw = 384;
 // One packet by one wave. img_in: payload (+ tag) as read; img_out: the result. Both also
 // serve as the MAC image (seal: the ciphertext in img_out; open: the ciphertext in img_in).
 __device__ void pp_packet(const Hdr& h, uint64_t ticket, const uint8_t* slot, uint8_t* out, uint64_t* done,
-                          uint4* img_in, uint4* img_out) {
+                          uint4* img_in, uint4* img_out, uint64_t* svc, uint64_t t_seen) {
   // ticket: the entry's seq (the caller's unique call number + 1), echoed in the completion word
   const uint32_t lane = threadIdx.x & 63u;
   const bool open = h.mode == WG_MODE_OPEN;
@@ -242,8 +244,11 @@ __device__ void pp_packet(const Hdr& h, uint64_t ticket, const uint8_t* slot, ui
   PP_STAMP(ticket, 5);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every result byte has landed before done
   PP_STAMP(ticket, 6);
-  if (lane == 0)
+  if (lane == 0) {
+    // the service time first: it is ordered before the completion word the caller polls for
+    __hip_atomic_store(svc, __builtin_amdgcn_s_memrealtime() - t_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(done, (ticket << 8) | status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // lane k's 64-bit value (k wave-uniform). readlane returns int: each half goes through uint32_t, or
@@ -299,9 +304,7 @@ __global__ void __launch_bounds__(64) k_pp(PPParams P) {
           pk &= pk - 1ull;
           const uint32_t i = 64u * (word0 + k) + bit;
           const uint8_t* slot = P.in + (size_t)i * kInSlot;
-#ifdef WG_PP_STAMPS
           const uint64_t t_seen = __builtin_amdgcn_s_memrealtime();
-#endif
           // header + payload prefix, loaded after the doorbell was seen (the host wrote them before
           // it): a system-scope acquire (no stale line of an earlier use of this slot survives in
           // the CU's caches), then 16-B loads per lane (system-scope dword loads go over PCIe one
@@ -320,7 +323,7 @@ __global__ void __launch_bounds__(64) k_pp(PPParams P) {
 #endif
           PP_STAMP(seq, 1);
           if (h.len <= kPPMaxLen && (h.mode == WG_MODE_SEAL || h.mode == WG_MODE_OPEN)) {
-            pp_packet(h, seq, slot, P.out + (size_t)i * kOutSlot, P.done + i, img_in, img_out);
+            pp_packet(h, seq, slot, P.out + (size_t)i * kOutSlot, P.done + i, img_in, img_out, P.svc + i, t_seen);
           } else if (lane == 0) {  // refused by the host before publishing; never expected here
             __hip_atomic_store(P.done + i, (seq << 8) | 0xffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           }
@@ -431,7 +434,9 @@ struct PPServer {
   volatile wgpp::Ctl* ctl() { return (volatile wgpp::Ctl*)(host + ctl_off()); }
   size_t exit_off() const { return ctl_off() + sizeof(wgpp::Ctl); }
   volatile uint64_t* exit_flag() { return (volatile uint64_t*)(host + exit_off()); }
-  size_t bytes() const { return exit_off() + 64; }
+  size_t svc_off() const { return exit_off() + 64; }
+  volatile uint64_t* svc(uint32_t i) { return (volatile uint64_t*)(host + svc_off()) + i; }
+  size_t bytes() const { return svc_off() + (size_t)wgpp::kRing * 8; }
 };
 
 void pp_free(PPServer* S) {
@@ -506,6 +511,7 @@ int pp_ensure(PPServer* S) {
   P.bell = (const uint64_t*)(S->dev + S->bell_off());
   P.ctl = (const wgpp::Ctl*)(S->dev + S->ctl_off());
   P.exit_flag = (uint64_t*)(S->dev + S->exit_off());
+  P.svc = (uint64_t*)(S->dev + S->svc_off());
   P.ack = S->d_ack;
   P.exited = S->d_exited;
   P.quit = S->d_exited + 1;
@@ -547,6 +553,22 @@ void pp_stop(wg_ctx* c) {
   (void)hipStreamSynchronize(S->stream);
   pp_free(S);
   delete S;
+}
+
+// Stages of the calling thread's last per-packet call (wg_pp_last_call): host steady-clock
+// nanoseconds, the device's service time from the entry's svc word, whether the caller slept on its
+// futex, and whether this call relaunched the server.
+struct PPCallStamps {
+  uint64_t t_enter = 0, t_claimed = 0, t_published = 0, t_complete = 0, t_exit = 0;
+  uint64_t svc_ticks = 0;
+  uint32_t slept = 0, relaunched = 0;
+};
+thread_local PPCallStamps g_pp_last;
+
+inline uint64_t pp_now_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
 }
 
 // Claim a free ring entry. Calls spread over the waves (call k prefers entry (k mod W) E +
@@ -670,17 +692,19 @@ int pp_sleep(PPServer* S, uint32_t i, uint64_t seq, uint64_t* d_out) {
 int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const uint8_t* src, uint32_t len,
               uint8_t* dst) {
   if (len > wgpp::kPPMaxLen) return pp_big(c, open, key_slot, counter, src, len, dst);
+  PPCallStamps& st = g_pp_last;
+  st = PPCallStamps{};
+  st.t_enter = pp_now_ns();
   PPServer* S;
   int rc;
   if ((rc = pp_get(c, &S)) != WG_OK) return rc;
   uint32_t key[8];
-  {
-    std::lock_guard<std::mutex> lk(c->keys_mu);
-    memcpy(key, c->keys_host.data() + (size_t)key_slot * 32, 32);
-  }
+  key_snapshot(c, key_slot, key);
   const uint64_t k = S->calls.fetch_add(1, std::memory_order_relaxed);
   const uint64_t seq = k + 1;  // unique per call: the completion word echoes it
   const uint32_t i = pp_claim(S, k);
+  st.t_claimed = pp_now_ns();
+  const uint64_t launches0 = S->launches.load(std::memory_order_relaxed);
   wgpp::Hdr* h = (wgpp::Hdr*)S->in_slot(i);
   h->seq = seq;
   h->counter = counter;
@@ -695,6 +719,7 @@ int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const u
   // publish: toggle the entry's doorbell bit (a locked RMW, ordered after every byte above)
   __atomic_fetch_xor(S->bell(i >> 6), 1ull << (i & 63u), __ATOMIC_SEQ_CST);
   rc = pp_ensure(S);
+  st.t_published = pp_now_ns();
   uint64_t d = 0;
   // with more calls in flight than spin_callers, a caller that polls for its whole round trip burns a
   // core the host does not have (and under a CPU quota every thread of the process then stalls until
@@ -705,6 +730,7 @@ int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const u
     d = __atomic_load_n((const uint64_t*)S->done(i), __ATOMIC_ACQUIRE);
     if ((d >> 8) == seq) break;
     if (spin > spin_limit) {  // past the usual round trip: sleep until the waker sees the completion
+      st.slept = 1;
       rc = pp_sleep(S, i, seq, &d);
       break;
     }
@@ -712,8 +738,11 @@ int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const u
     __builtin_ia32_pause();
   }
   S->active.fetch_sub(1, std::memory_order_relaxed);
+  st.t_complete = pp_now_ns();
+  st.relaunched = S->launches.load(std::memory_order_relaxed) != launches0 ? 1u : 0u;
   int result = rc;
   if (rc == WG_OK) {
+    st.svc_ticks = *S->svc(i);
     const uint32_t status = (uint32_t)(d & 0xffu);
     if (status == WG_PKT_OK) {
       if (open) {
@@ -733,6 +762,7 @@ int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const u
     // completion word has landed, so the entry is never lost
     S->state[i].store(kOrphan, std::memory_order_release);
   }
+  st.t_exit = pp_now_ns();
   return result;
 }
 
@@ -752,6 +782,22 @@ int wg_open1(wg_ctx* c, uint32_t key_slot, uint64_t counter, const uint8_t* in, 
   if (len > WG_MAX_PACKET) return fail(WG_E2BIG, "packet of %u bytes", len);
   if (key_slot >= c->key_slots) return fail(WG_ERANGE, "key slot %u", key_slot);
   return pp_submit(c, true, key_slot, counter, in, len, pt);
+}
+
+// Stages of the calling thread's last wg_seal1 / wg_open1 (a diagnostic for latency outliers,
+// tools/batcher_bench stamps=1), in nanoseconds: out[0] total, [1] claim (key snapshot + ring entry),
+// [2] publish (header and payload copy + doorbell + server check), [3] wait (published -> completion
+// observed by the caller, spinning or woken), [4] device service (the wave's doorbell sighting ->
+// completion store), [5] copy-out and release, [6] slept on the futex (0/1), [7] this call relaunched
+// the server (0/1). Packets past a ring slot (the host batch path) leave zeros.
+int wg_pp_last_call(uint64_t* out, uint32_t n) {
+  if (!out && n) return fail(WG_EINVAL, "NULL argument");
+  const PPCallStamps& s = g_pp_last;
+  const uint64_t v[8] = {s.t_exit - s.t_enter, s.t_claimed - s.t_enter, s.t_published - s.t_claimed,
+                         s.t_complete - s.t_published, s.svc_ticks * 10u, s.t_exit - s.t_complete, s.slept,
+                         s.relaunched};
+  for (uint32_t k = 0; k < n && k < 8u; ++k) out[k] = s.t_enter ? v[k] : 0u;
+  return WG_OK;
 }
 
 int wg_pp_config(wg_ctx* c, uint32_t waves, uint32_t idle_us) {

@@ -181,6 +181,13 @@ struct wg_queue {
   uint8_t* z_in = nullptr;   // device alias
   uint8_t* h_out = nullptr;  // pinned ring: results (ct || tag, or plaintext)
   uint8_t* z_out = nullptr;
+  // pinned, device-mapped: the key of each ring slot, copied from the context's key mirror when the
+  // packet is submitted. The kernel reads the key with the packet (its descriptor's key_slot is the
+  // ring slot), so wg_keys_zero / wg_keys_set after a submit cannot change what a queued packet is
+  // sealed or opened with, exactly as a synchronous cipher() before clean() used the old key.
+  uint32_t* h_key = nullptr;
+  uint32_t* z_key = nullptr;
+  uint64_t submit_timeout_ns = 0;  // wg_queue_set_submit_timeout: 0 = a submit waits for a free slot without bound
   std::unique_ptr<wgq::SlotMeta[]> meta;
   wgq::IdQueue done_q;                // completions: pushed by the dispatcher, popped by consumers
   uint32_t lanes = 0, per_lane = 0;     // producer lanes and the ring slots each owns
@@ -211,16 +218,19 @@ namespace {
 // One launch per batch: the kernel reads the batch's descriptors straight from pinned memory (no
 // copy), one packet per slot (WG_F_UNIFORM is only a scheduling hint: a queue batch is small, so no
 // longest-first ordering launches are worth their cost).
+// The launch takes the queue's own per-slot key table (OwnKeys): the transport kernel whatever kernel
+// the context selects, no plan workspace and no timing events, so the dispatcher needs no c->mu.
 int queue_launch(wg_queue* q, wgq::Batch& b, uint32_t lmax) {
   wg_ctx* c = q->c;
   const uint64_t size = (uint64_t)q->cap * q->stride;
+  const OwnKeys ok{q->z_key, q->cap};
   int rc;
   if (q->mode == WG_MODE_SEAL)
     rc = launch_transport<WG_MODE_SEAL>(c, b.z_desc, b.n, q->z_in, size, q->z_out, size, nullptr, lmax, WG_F_UNIFORM,
-                                        q->stream, nullptr, &q->lpt_hist, &q->lpt_order);
+                                        q->stream, nullptr, &q->lpt_hist, &q->lpt_order, false, &ok);
   else
     rc = launch_transport<WG_MODE_OPEN>(c, b.z_desc, b.n, q->z_in, size, q->z_out, size, b.z_status, lmax,
-                                        WG_F_UNIFORM, q->stream, nullptr, &q->lpt_hist, &q->lpt_order);
+                                        WG_F_UNIFORM, q->stream, nullptr, &q->lpt_hist, &q->lpt_order, false, &ok);
   if (rc != WG_OK) return rc;
   HIPTRY(hipEventRecord(b.done, q->stream));
   return WG_OK;
@@ -282,7 +292,7 @@ void queue_dispatch(wg_queue* q) {
           d.out_off = (uint64_t)s * q->stride;
           d.counter = m.counter;
           d.len = m.len;
-          d.key_slot = m.key_slot;
+          d.key_slot = s;  // the key copied into the ring slot at submit time
           if (fill->n == 0) first_ns = wgq::now_ns();
           fill->slots[fill->n++] = s;
           lmax = std::max(lmax, m.len);
@@ -336,6 +346,10 @@ void queue_free(wg_queue* q) {
   }
   if (q->h_in) (void)hipHostFree(q->h_in);
   if (q->h_out) (void)hipHostFree(q->h_out);
+  if (q->h_key) {
+    memset(q->h_key, 0, (size_t)q->cap * 32);  // no session key outlives the queue in pinned memory
+    (void)hipHostFree(q->h_key);
+  }
   q->lpt_hist.release();
   q->lpt_order.release();
   if (q->stream) (void)hipStreamDestroy(q->stream);
@@ -405,10 +419,18 @@ int queue_submit(wg_queue* q, int mode, uint32_t key_slot, uint64_t counter, con
   if (const int e = q->err.load(std::memory_order_relaxed)) return fail(e, "queue failed earlier");
   wgq::Lane& ln = q->lane[wgq::thread_number() % q->lanes];
   uint32_t s = 0;
+  uint64_t deadline = 0;  // wg_queue_set_submit_timeout: WG_EAGAIN once no slot was free for that long
   for (uint32_t round = 0;; ++round) {
     const uint32_t w = q->wake_word.load(std::memory_order_acquire);
     const int r = queue_try_slot(q, ln, &s);
     if (r == 1) break;
+    if (q->submit_timeout_ns) {
+      const uint64_t now = wgq::now_ns();
+      if (!deadline) deadline = now + q->submit_timeout_ns;
+      else if (now >= deadline)
+        return fail(WG_EAGAIN, "no free queue slot for %llu us (is the consumer calling wg_reap_done?)",
+                    (unsigned long long)(q->submit_timeout_ns / 1000u));
+    }
     // this lane's ready ring is full (the dispatcher is about to gather it), or every slot is in use:
     // wait for wg_reap_done without burning the CPU the consumers need to free them
     if (round < 2 || r == 2) {
@@ -425,6 +447,7 @@ int queue_submit(wg_queue* q, int mode, uint32_t key_slot, uint64_t counter, con
     futex(&q->wake_word, FUTEX_WAIT_PRIVATE, w, &ts);
     q->free_waiters.fetch_sub(1, std::memory_order_relaxed);
   }
+  key_snapshot(q->c, key_slot, q->h_key + 8ull * s);
   wgq::SlotMeta& m = q->meta[s];
   m.user = user;
   m.counter = counter;
@@ -511,11 +534,14 @@ int wg_queue_create(wg_ctx* c, int mode, uint32_t capacity, uint32_t max_len, ui
   const size_t ring = (size_t)q->cap * q->stride;
   bool ok = hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking) == hipSuccess &&
             hipHostMalloc((void**)&q->h_in, ring, hipHostMallocMapped | hipHostMallocPortable) == hipSuccess &&
-            hipHostMalloc((void**)&q->h_out, ring, hipHostMallocMapped | hipHostMallocPortable) == hipSuccess;
+            hipHostMalloc((void**)&q->h_out, ring, hipHostMallocMapped | hipHostMallocPortable) == hipSuccess &&
+            hipHostMalloc((void**)&q->h_key, (size_t)q->cap * 32, hipHostMallocMapped | hipHostMallocPortable) ==
+                hipSuccess;
   if (ok) {
     q->z_in = mapped_alias(q->h_in);
     q->z_out = mapped_alias(q->h_out);
-    ok = q->z_in && q->z_out;
+    q->z_key = (uint32_t*)mapped_alias(q->h_key);
+    ok = q->z_in && q->z_out && q->z_key;
   }
   q->batches.resize(q->inflight);
   for (auto& b : q->batches) {
@@ -639,6 +665,12 @@ int wg_reap_done(wg_queue* q, const wg_completion* done, uint32_t n) {
     q->wake_word.fetch_add(1, std::memory_order_release);
     futex(&q->wake_word, FUTEX_WAKE_PRIVATE, INT32_MAX, nullptr);
   }
+  return WG_OK;
+}
+
+int wg_queue_set_submit_timeout(wg_queue* q, uint32_t timeout_us) {
+  if (!q) return fail(WG_EINVAL, "NULL queue");
+  q->submit_timeout_ns = 1000ull * timeout_us;
   return WG_OK;
 }
 

@@ -70,6 +70,12 @@ struct RxState {
   DevBuf d_pos;             // per packet: its (slot, counter) entry in d_tab, or ~0
   DevBuf d_flag;            // the order flag, k_rp_judge's finished blocks and groups, 64 B apart (0 between calls)
   bool five = false;        // WG_RX_LAUNCHES=5: decide and advance as two launches (A/B)
+  // test hooks (tests/test_gpu_rx.py::test_replay_flag_protocol_under_block_skew), never set in production:
+  // WG_RX_TEST_SKEW=us delays every block but block 0 of each replay launch by `us` before it reads
+  // the order flag, the done counts or the new tops; WG_RX_TEST_MUTANT=1 restores round 4's flag
+  // clearing (k_rp_fixmark clears the word its own later blocks read) so the test can show it fails
+  uint32_t test_skew_ticks = 0;  // s_memrealtime ticks (100 MHz)
+  bool test_mutant = false;
   uint64_t checks = 0;      // replay checks queued: the order flag alternates between two words
   hipEvent_t ev = nullptr;  // last use of the replay scratch, and its stream (stream-ordered reuse)
   hipStream_t ev_stream = (hipStream_t)-1;
@@ -122,6 +128,8 @@ int rx_get(wg_ctx* c, RxState** out) {
   if (!c->rx) {
     c->rx = new RxState();
     if (const char* e = getenv("WG_RX_LAUNCHES")) c->rx->five = atoi(e) == 5;
+    if (const char* e = getenv("WG_RX_TEST_SKEW")) c->rx->test_skew_ticks = 100u * (uint32_t)std::max(0, atoi(e));
+    if (const char* e = getenv("WG_RX_TEST_MUTANT")) c->rx->test_mutant = atoi(e) != 0;
   }
   *out = c->rx;
   return WG_OK;
@@ -212,7 +220,25 @@ struct RxParams {
   uint32_t* unsorted;  // 0 while the batch's (slot, counter) pairs strictly increase with the index
   uint32_t* unsorted_next;  // the next check's flag word (checks alternate between two words)
   uint32_t* done_blocks;  // k_rp_judge: blocks finished (0 between calls)
+  uint32_t skew_ticks;    // test hook WG_RX_TEST_SKEW (0 in production)
+  uint32_t mutant;        // test hook WG_RX_TEST_MUTANT (0 in production)
 };
+
+// Test hook: every block but block 0 waits skew_ticks (s_memrealtime, 100 MHz) before it touches the
+// check's shared words, so block 0 runs its whole part first. A protocol in which an early block
+// clears or consumes a word a later block of the same launch still reads then fails every time.
+__device__ __forceinline__ void rx_test_skew(const RxParams& P) {
+  if (P.skew_ticks == 0u || blockIdx.x == 0u) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)P.skew_ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+// Words shared between launches are reset with device-scope (agent) atomic stores: they bypass the
+// XCD's L2, like the atomics that read and raise them, so no write-back of that L2 is needed for
+// another XCD's blocks of the next launch to see the reset.
+__device__ __forceinline__ void reset_word(uint32_t* p) {
+  __hip_atomic_store(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -500,6 +526,14 @@ __device__ __forceinline__ void rp_advance_all(const RxParams& P) {
 
 // Counts the calling block done once every atomic it issued has completed; true in the last block
 // of the grid (whose device-scope loads then see every block's new tops; no cache flush needed).
+// Ordering, per the LLVM AMDGPU memory model for GFX942/GFX950: the blocks exchange data only through
+// agent-scope atomics (atomicMax on the new tops, atomicAdd on the counters, relaxed agent-scope
+// atomic loads of the new tops), which the hardware performs past the XCD's non-coherent L2. An
+// agent-scope release before the counter add is `buffer_wbl2 sc1; s_waitcnt vmcnt(0)`; the write-back
+// is for plain stores held in that L2, and this protocol has none, so `s_waitcnt vmcnt(0)` (every
+// atomic of this thread acknowledged) + the barrier is the release, and the acquire side needs no L2
+// invalidate because the last block reads the new tops with atomic loads. (Round 4 measured the
+// agent-scope fences that a grid barrier needs at 156 us per check: DESIGN.md §8.)
 // Two levels (kTopWays groups of blocks, then the groups): a counter that every block of a 256-block
 // grid raises serialises 256 same-address atomics; each counter sits on its own 64-B line.
 __device__ __forceinline__ bool rp_last_block(const RxParams& P) {
@@ -512,7 +546,7 @@ __device__ __forceinline__ bool rp_last_block(const RxParams& P) {
     uint32_t* gc = P.done_blocks + 16u * (1u + g);
     last = false;
     if (atomicAdd(gc, 1u) == members - 1u) {
-      *gc = 0u;  // every member has arrived: ready for the next check (the kernel boundary orders it)
+      reset_word(gc);  // every member has arrived: ready for the next check (the kernel boundary orders it)
       last = atomicAdd(P.done_blocks, 1u) == groups - 1u;
     }
   }
@@ -528,6 +562,7 @@ __device__ __forceinline__ bool rp_last_block(const RxParams& P) {
 // more than a launch.)
 __global__ void __launch_bounds__(256) k_rp_order(RxParams P) { rp_order_at(P, blockIdx.x * 256u + threadIdx.x); }
 __global__ void __launch_bounds__(256) k_rp_insert(RxParams P) {
+  rx_test_skew(P);
   rp_insert_at(P, blockIdx.x * 256u + threadIdx.x, *P.unsorted != 0);
 }
 __global__ void __launch_bounds__(256) k_rp_decide(RxParams P) {
@@ -540,11 +575,12 @@ __global__ void __launch_bounds__(256) k_rp_advance(RxParams P) { rp_advance_at(
 // With `advance` its last block moves every slot's window.
 __global__ void __launch_bounds__(256) k_rp_judge(RxParams P, uint32_t advance) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  rx_test_skew(P);
   rp_order_at(P, i);
   rp_decide_at(P, i, false);
   if (!advance || !rp_last_block(P)) return;
   rp_advance_all(P);
-  if (threadIdx.x == 0) *P.done_blocks = 0u;
+  if (threadIdx.x == 0) reset_word(P.done_blocks);
 }
 // After k_rp_insert (a no-op for a strictly increasing batch): copies of a pair other than its
 // lowest index become REPLAY, then the ring bits of the accepted counters; each used table entry is
@@ -553,6 +589,7 @@ __global__ void __launch_bounds__(256) k_rp_judge(RxParams P, uint32_t advance) 
 __global__ void __launch_bounds__(256) k_rp_fixmark(RxParams P) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   bool own_entry = false;
+  rx_test_skew(P);
   if (*P.unsorted && i < P.n && P.pos[i] != ~0u) {
     own_entry = P.tab[P.pos[i]] == i;
     if (!own_entry && P.status[i] == WG_PKT_OK) P.status[i] = WG_PKT_REPLAY;
@@ -561,12 +598,12 @@ __global__ void __launch_bounds__(256) k_rp_fixmark(RxParams P) {
   if (own_entry) P.tab[P.pos[i]] = ~0u;
   // the next check's flag, not this one's: every thread of this launch reads this check's flag, and
   // a block that starts after thread 0 has cleared it would skip its fix-ups
-  if (i == 0) *P.unsorted_next = 0u;
+  if (i == 0) reset_word(P.mutant ? P.unsorted : P.unsorted_next);
 }
 __global__ void __launch_bounds__(256) k_rp_mark(RxParams P) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
   rp_mark_at(P, i);
-  if (i == 0) *P.unsorted = 0u;  // k_rp_decide was its last reader: 0 again for the next batch
+  if (i == 0) reset_word(P.unsorted);  // k_rp_decide was its last reader: 0 again for the next batch
 }
 
 // keepalive / IP version / AllowedIPs, one thread per packet (wgt::rx_verdict, shared with the
@@ -763,6 +800,8 @@ int wg_rx_check(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* pt, ui
     P.unsorted_next = (uint32_t*)r->d_flag.p + ((r->checks + 1u) & 1u);
     ++r->checks;
     P.done_blocks = (uint32_t*)r->d_flag.p + 16;  // its own line; group counters on the next lines
+    P.skew_ticks = r->test_skew_ticks;
+    P.mutant = r->test_mutant ? 1u : 0u;
     if (!r->five) {
       const bool inl = c->key_slots <= kAdvanceInline;
       hipLaunchKernelGGL(wgrx::k_rp_judge, dim3(grid), dim3(256), 0, s, P, inl ? 1u : 0u);

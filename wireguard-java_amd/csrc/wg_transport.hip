@@ -122,6 +122,8 @@ struct TransportParams {
   const RxTables* rx;     // open with WG_F_RX_FILTER: receive-side verdict in the status (else NULL)
   const uint32_t* n_long; // k_*_mixed: device count of the packets at the front of the order that take
                           // 16-lane slots (written by k_lpt_scatter); NULL otherwise
+  uint32_t test_flip;     // test hook (WG_TEST_STEP_FLIP=N, k_step only): N > 0 flips bit 0 of the sealed tag of
+                          // each slot's first packet when its index is a multiple of N (a power of two); 0 in production
 #ifdef WG_DIAG
   uint64_t* stamps;       // diagnostic build only: 10 x u64 per wave (cycles per phase, start/end times)
 #endif
@@ -864,6 +866,25 @@ k_duplex(TransportParams S, TransportParams O, uint32_t seal_blocks, uint32_t op
 // that holds at most half the resident waves anyway (the persistent longest-first pairs of a
 // mixed batch: 4 waves per SIMD), which takes the WPE = 4 build (66 VGPRs and no SGPR spills,
 // against 64 VGPRs and 12 SGPRs spilled to VGPR lanes; WG_STEP_WPE4=0 for the other).
+// Test hook of k_step (WG_TEST_STEP_FLIP, never set in production): between the two halves, lane 0 of
+// each slot flips bit 0 of the tag its seal wrote for the slot's first packet (batch position g) when
+// that packet's index is a multiple of S.test_flip. The open half then rejects it and the ciphertext
+// differs from the reference, so the bench's check of the k_step output it timed must fail
+// (tests/test_gpu_bench.py). Outside transport_body: the product body's code is unchanged.
+template <int G>
+__device__ __forceinline__ void step_test_flip(const TransportParams& S, uint32_t blk, uint32_t wv) {
+  const uint32_t lane = threadIdx.x & 63u, g = (blk * TW + wv) * (64u / G) + lane / G;
+  if ((lane & (G - 1u)) == 0u && g < S.n) {
+    const uint32_t i = S.order ? S.order[g] : g;
+    const wg_pkt d = S.desc[i];
+    if ((i & (S.test_flip - 1u)) == 0u &&
+        transport_valid<WG_MODE_SEAL>(d.in_off, d.out_off, d.len, d.key_slot, S.max_len, S.key_slots, S.in_size,
+                                      S.out_size))
+      S.out[d.out_off + d.len] ^= 1u;
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
+}
+
 template <int G = 8, int WPE = 8>
 __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_step(TransportParams S, TransportParams O) {
@@ -875,6 +896,7 @@ k_step(TransportParams S, TransportParams O) {
   // the open reads the ciphertext and tags this wave just stored: wait until the stores are
   // performed and drop this CU's L1 lines (an in-place seal read the plaintext through them)
   asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
+  if (S.test_flip) step_test_flip<G>(S, blockIdx.x, wv);
   transport_body<WG_MODE_OPEN, G>(O, blockIdx.x, wv, img_[wv], rec_[wv], iter);
 }
 

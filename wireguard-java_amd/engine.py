@@ -396,6 +396,11 @@ class Queue:
         L.check(self._lib.wg_reap_done(self.q, self._buf, n))
         return out
 
+    def set_submit_timeout(self, timeout_us: int) -> None:
+        """wg_queue_set_submit_timeout: submit() raises WgError(EAGAIN) once no slot has been free for
+        timeout_us (0: it waits without bound, the default)."""
+        L.check(self._lib.wg_queue_set_submit_timeout(self.q, timeout_us))
+
     def stats(self) -> tuple[int, int]:
         a, b = ctypes.c_uint64(), ctypes.c_uint64()
         L.check(self._lib.wg_queue_stats(self.q, ctypes.byref(a), ctypes.byref(b)))

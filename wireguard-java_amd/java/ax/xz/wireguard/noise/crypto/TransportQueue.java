@@ -71,6 +71,21 @@ public final class TransportQueue implements AutoCloseable {
 		}
 	}
 
+	/**
+	 * How long submit() waits for a free ring slot before it fails (wg_queue_set_submit_timeout; WG_EAGAIN,
+	 * thrown as a RuntimeException by WgAead.check): a stalled UDP / tun worker then cannot block every
+	 * ForkJoinPool worker for good. 0 (the default): wait without bound.
+	 */
+	public void submitTimeout(int timeoutUs) {
+		try {
+			WgAead.check((int) WgAead.QUEUE_SUBMIT_TIMEOUT.invokeExact(q, timeoutUs));
+		} catch (RuntimeException e) {
+			throw e;
+		} catch (Throwable e) {
+			throw new RuntimeException(e);
+		}
+	}
+
 	/** Up to reapMax finished packets (waits up to timeoutUs for the first); read them with user/data/status. */
 	public int reap(int max, int timeoutUs) {
 		try {
