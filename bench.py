@@ -37,9 +37,9 @@ The JSON line also carries:
                 `roofline.step` the timed K-stream steps (`value` comes from those)
   cpu_baseline  the CPU restatement (oracle/liboracle.so, bit-exact to the
                 reference) timed on this host's cores, rank 0, N = 1 only
-  oracle_sample ct||tag of 2048 seeded packets of the timed batch against the oracle (rank 0,
-                N = 1), gathered right after the timed region from the buffers the timed launches
-                wrote (poisoned before it); a mismatch makes `verified` false
+  oracle_sample ct||tag of 2048 seeded packets of the timed batch against the oracle (every rank,
+                its own shard), gathered right after the timed region from the buffers the timed
+                launches wrote (poisoned before it); a mismatch on any rank makes `verified` false
 Before the W warmup steps every rank runs untimed steps for --ramp-ms (default 150 ms)
 so the GPU clocks have ramped before the timed region (ramp_ms in the JSON line).
 """
@@ -359,6 +359,10 @@ def main():
     # kernel traces, where the profiler makes each host enqueue slower than a step)
     ap.add_argument("--graph", action="store_true")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
+    # multi-rank rehearsal on a one-GPU box (not the metric's configuration): the report's collectives
+    # over gloo instead of RCCL, and every rank on cuda:0 with its own wg_ctx (tests/test_gpu_dist.py)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"], help=argparse.SUPPRESS)
+    ap.add_argument("--same-device", action="store_true", help=argparse.SUPPRESS)
     # diagnostic knobs (not the metric's configuration): batch size and session count of C1 / C2
     ap.add_argument("--packets", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--keys", type=int, default=0, help=argparse.SUPPRESS)
@@ -381,11 +385,17 @@ def main():
     # under torchrun (WORLD_SIZE set) the ranks always form an RCCL group, one rank included, so the
     # rendezvous, barriers and gathers of the multi-GPU line run on the GPU path at any N
     use_dist = "WORLD_SIZE" in os.environ
+    if args.same_device:
+        local = 0
     if use_dist:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    rdev = dev if args.dist_backend == "nccl" else "cpu"  # where the report's reductions run
 
     wg = importlib.import_module("wireguard-java_amd")
     lengths, slots, counters, nkeys, wdesc, uniform = build_workload(args.workload, rank, world, args.packets, args.keys)
@@ -541,10 +551,10 @@ def main():
         ok_data = bool(torch.equal(back[mask], pt[mask]))
         del idx, pkt, mask
 
-    # a seeded sample of the timed batch, copied out for the oracle check (rank 0, N = 1, next to the
-    # CPU baseline; the oracle is the checker, never the thing measured)
+    # a seeded sample of the timed batch, copied out for the oracle check (every rank checks its own
+    # shard; the oracle is the checker, never the thing measured)
     sample = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if not args.no_cpu_baseline:
         pick = np.sort(np.random.default_rng(4242).choice(n, min(n, 2048), replace=False))
         sd = desc[pick].copy()
         SS = S[pick]
@@ -598,6 +608,10 @@ def main():
     copy_ms = train(lambda: back.copy_(pt))
     copy_gbs = 2.0 * pt.numel() / (copy_ms * 1e-3) / 1e9
 
+    # the oracle check of this rank's sample (before the reductions: a mismatch on any rank fails the line)
+    sample_res = oracle_sample_check(sample, keys) if sample is not None else None
+    sample_ok = sample_res is None or sample_res["bit_exact"]
+
     payload = 2.0 * float(lengths.sum())  # sealed + opened bytes per step on this rank
     D = importlib.import_module("wireguard-java_amd.dist")
     # transport kernel launches per step: k_duplex, or k_step (one WG_F_AFTER_SEAL step), or seal + open
@@ -605,15 +619,15 @@ def main():
     launches = (1 if (args.mode == "duplex" or fused_step) else 2) * (K if args.mode != "duplex" else 1)
     # this rank's own figures, gathered before the max-over-ranks reduction (BASELINE configs[3]:
     # per-GPU and aggregate GiB/s)
-    per_gpu = D.gather_per_rank(dist if use_dist else None, dev, {
+    per_gpu = D.gather_per_rank(dist if use_dist else None, rdev, {
         "elapsed_s": elapsed, "payload_bytes": payload * args.steps, "packets": n, "seal_ms": seal_ms,
         "open_ms": open_ms, "kernel_ms": gpu_step_ms / launches})
     if use_dist:
         (elapsed, seal_ms, open_ms, gpu_step_ms), payload_all, all_ok = D.reduce_report(
-            dist, dev, [elapsed, seal_ms, open_ms, gpu_step_ms], payload, ok_status and ok_data)
+            dist, rdev, [elapsed, seal_ms, open_ms, gpu_step_ms], payload, ok_status and ok_data and sample_ok)
     else:
         payload_all = payload
-        all_ok = ok_status and ok_data
+        all_ok = ok_status and ok_data and sample_ok
 
     value = payload_all * args.steps / elapsed / GIB
     # seal reads L, writes L+16; open reads L+16, writes L -> 4L+32 per packet
@@ -661,7 +675,9 @@ def main():
             "data": "synthetic (random payload in HBM, splitmix64 keys, sequential counters)",
             "config": {"workload": wdesc, "packets_per_gpu": n, "payload_bytes": int(lengths.mean()), "step": args.mode,
                        "streams": K,
-                       "sessions_per_gpu": nkeys, "parallelism": f"dp{world} sharded by session, no collective"},
+                       "sessions_per_gpu": nkeys, "parallelism": f"dp{world} sharded by session, no collective",
+                       **({"rehearsal": f"{world} ranks on cuda:0, report over {args.dist_backend}"}
+                          if args.same_device else {})},
             "roofline": {"bound": "hbm", "kernel": kname + (", one stream" if single_ms is not None else ""),
                          "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -687,12 +703,10 @@ def main():
             line["valu_roofline"] = {"insts_per_launch": round(valu), "achieved": round(rate / 1e12, 4),
                                      "peak": round(VALU_PEAK_WIPS / 1e12, 4), "unit": "T wave-instr/s",
                                      "frac": round(rate / VALU_PEAK_WIPS, 4), "source": "SQ_INSTS_VALU, profiles/pmc_*.json"}
+        if sample_res is not None:
+            line["oracle_sample"] = dict(sample_res, ranks=world, all_ranks_verified=bool(all_ok))
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(lengths, slots, counters, keys)
-            line["oracle_sample"] = oracle_sample_check(sample, keys)
-            if not line["oracle_sample"]["bit_exact"]:
-                all_ok = False
-                line["verified"] = False
         print(json.dumps(line), flush=True)
     eng.close()
     if use_dist:

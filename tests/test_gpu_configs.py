@@ -94,6 +94,50 @@ def test_c2_full_every_packet(engine, path):
     assert np.array_equal(b, want)
 
 
+@pytest.mark.parametrize("n", [65536, 131072, 50000])
+def test_k_step_claim_every_packet(n):
+    """WG_CLAIM=1: mixed-length WG_F_AFTER_SEAL steps through k_step_claim, whose slots claim their
+    packets dynamically from 64 interleaved longest-first sub-orders and whose open half replays the
+    seal half's log. Three steps in a row (the counters are reset by every step's k_lpt_scatter): every
+    ct || tag against the oracle, every plaintext against the input, every status OK. n = 50,000 takes
+    a grid that 64 does not divide (fewer sub-orders)."""
+    import os
+    torch, dev = _dev()
+    W = wg()
+    old = os.environ.get("WG_CLAIM")
+    os.environ["WG_CLAIM"] = "1"
+    try:
+        eng = W.Engine(0, key_slots=256)
+    finally:
+        if old is None:
+            del os.environ["WG_CLAIM"]
+        else:
+            os.environ["WG_CLAIM"] = old
+    try:
+        lengths, S, off, total, desc = _c2_batch(W, n)
+        keys = splitmix_np(0xC1A1, 32 * 256)
+        pt = splitmix_np(0x5EED2028 + n, total)
+        eng.set_keys(0, keys.tobytes())
+        d = torch.from_numpy(W.desc_as_int64(desc)).to(dev)
+        dpt = torch.from_numpy(pt).to(dev)
+        ref = np.zeros(total, np.uint8)
+        O.seal_batch(desc, pt, ref, keys, threads=16)
+        want = pt.copy()
+        for i in range(n):
+            want[int(off[i]) + int(lengths[i]):int(off[i]) + int(S[i])] = 0
+        for rep in range(3):
+            dct = torch.zeros(total, dtype=torch.uint8, device=dev)
+            back = torch.zeros(total, dtype=torch.uint8, device=dev)
+            st = torch.full((n,), 7, dtype=torch.int32, device=dev)
+            eng.duplex(d, dpt, dct, 9000, d, dct, back, st, 9000, uniform=False, after_seal=True)
+            torch.cuda.synchronize()
+            assert np.array_equal(dct.cpu().numpy(), ref), rep
+            assert int(st.abs().sum().item()) == 0, rep
+            assert np.array_equal(back.cpu().numpy(), want), rep
+    finally:
+        eng.close()
+
+
 @pytest.mark.parametrize("path", ["separate", "after_seal"])
 def test_c3_sharded_roundtrip_and_oracle_subset(path):
     """configs[3] on one GPU: 8M x 1420 B, session s -> rank s mod world (world 1 here),

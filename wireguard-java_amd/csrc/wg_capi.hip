@@ -112,6 +112,9 @@ struct wg_ctx {
   // half-occupancy k_step grids (C2's longest-first pairs) take the build allocated for 4 waves per
   // SIMD: no SGPR spills, C2 +0.7% in 3 alternations (profiles/r04_wpe_ab.txt); WG_STEP_WPE4=0: not
   bool step_wpe4 = true;
+  // mixed-length WG_F_AFTER_SEAL steps through k_step_claim (dynamic claims over the longest-first
+  // order) instead of the static snake (WG_CLAIM=1; A/B)
+  bool claim = false;
   // test hook WG_TEST_STEP_FLIP=N (power of two): the k_step launch's seal half writes a wrong tag for every
   // packet whose index is a multiple of N (tests/test_gpu_bench.py: the bench must report verified false)
   uint32_t test_flip = 0;
@@ -119,6 +122,7 @@ struct wg_ctx {
   DevBuf plan_nb, plan_prefix, plan_tiles, plan_ntiles, plan_tmp, lpt_hist, lpt_order;
   DevBuf lpt_hist2, lpt_order2;  // the open half of a wg_duplex_batch
   DevBuf lpt_nlong;              // k_lpt_scatter -> k_*_mixed: long packets at the front of lpt_order
+  DevBuf lpt_claim, lpt_chain;   // k_step_claim: sub-order counters (64-B lines) and the seal half's per-position log
 
   int kern = KERN_TRANSPORT;
   // host-API staging
@@ -350,7 +354,8 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
                    uint64_t out_size, uint32_t* status, uint32_t max_len, uint32_t flags, hipStream_t s,
                    uint64_t cap_waves, uint32_t G, DevBuf& lpt_hist, DevBuf& lpt_order, wgt::TransportParams* Pout,
                    uint32_t* grid_out, bool* ordered_out, const wgt::RxTables* rx = nullptr,
-                   bool private_ws = false, bool reuse_order = false, uint32_t split = 0) {
+                   bool private_ws = false, bool reuse_order = false, uint32_t split = 0,
+                   uint32_t* claim = nullptr, uint32_t claim_nc = 0) {
   bool ordered = false;
   wgt::TransportParams P{};
   P.desc = desc;
@@ -392,6 +397,11 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   const uint32_t waves = (uint32_t)((n + spw * per_slot - 1) / (spw * per_slot));
   const uint32_t grid = mixed ? (n + 4u * wgt::TW - 1u) / (4u * wgt::TW) + 2u : (waves + wgt::TW - 1) / wgt::TW;
   P.slots = grid * wgt::TW * spw;
+  if (claim) {
+    P.claim = claim;
+    P.claim_nc = claim_nc;
+    P.claim_base = P.slots / claim_nc;
+  }
   // mixed lengths: the rounds a slot runs, spread over the 4 issue-priority levels (k_transport),
   // so the waves that have done the least work issue first (C2 +2%); uniform batches keep the
   // default oldest-first arbitration (the same schedule cost C1 2%)
@@ -415,7 +425,7 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
       hipLaunchKernelGGL((wgt::k_lpt_hist<MODE>), dim3(lgrid), dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len, bh);
       hipLaunchKernelGGL((wgt::k_lpt_scatter<MODE>), dim3(lgrid), dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len,
                          (const uint32_t*)bh, (uint32_t*)lpt_order.p, split,
-                         mixed ? (uint32_t*)c->lpt_nlong.p : nullptr);
+                         mixed ? (uint32_t*)c->lpt_nlong.p : nullptr, claim, claim_nc, P.claim_base);
       HIPTRY(hipGetLastError());
     }
     P.order = (const uint32_t*)lpt_order.p;
@@ -585,9 +595,25 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
     wgt::TransportParams PS{}, PO{};
     uint32_t gs = 0, go = 0;
     bool os = false, oo = false;
+    // dynamic claims (WG_CLAIM): mixed lengths on the persistent 8-lane plan, with a grid that the
+    // sub-order count divides (claim_nc: the largest power of two <= 64 dividing it)
+    uint32_t claim_nc = 0;
+    if (c->claim && !(sb->flags & WG_F_UNIFORM) && sp.split == 0 && G == 8) {
+      const uint32_t spw = 8u;
+      const uint64_t cap_slots = spw * cap;
+      const uint64_t per_slot = 2ull * sb->n > cap_slots ? 2 * ((sb->n + cap_slots - 1) / cap_slots) : 1;
+      const uint32_t waves = (uint32_t)((sb->n + spw * per_slot - 1) / (spw * per_slot));
+      const uint32_t grid = (waves + wgt::TW - 1) / wgt::TW;
+      claim_nc = 64;
+      while (claim_nc > 1 && grid % claim_nc) claim_nc >>= 1;
+      if (per_slot < 2 || (rc = c->lpt_claim.ensure(64u * 64u)) != WG_OK ||
+          (rc = c->lpt_chain.ensure(sizeof(uint2) * (size_t)sb->n)) != WG_OK)
+        claim_nc = 0;
+    }
     rc = plan_transport<WG_MODE_SEAL>(c, sb->desc, sb->n, sb->in, sb->in_size, sb->out, sb->out_size, nullptr,
                                       sb->max_len, sb->flags, s, cap, G, c->lpt_hist, c->lpt_order, &PS, &gs, &os,
-                                      nullptr, true, false, sp.split);
+                                      nullptr, true, false, sp.split, claim_nc ? (uint32_t*)c->lpt_claim.p : nullptr,
+                                      claim_nc);
     if (rc == WG_OK)
       rc = plan_transport<WG_MODE_OPEN>(c, ob->desc, ob->n, ob->in, ob->in_size, ob->out, ob->out_size, ob->status,
                                         ob->max_len, ob->flags & ~WG_F_AFTER_SEAL, s, cap, G, c->lpt_hist,
@@ -595,6 +621,11 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
     // one issue-priority schedule over the seal and open halves (the rounds of both)
     if (PS.prio_step) PS.prio_step = PO.prio_step = 2u * PS.prio_step;
     PS.test_flip = c->test_flip;
+    if (claim_nc) {
+      PS.chain_out = (uint2*)c->lpt_chain.p;
+      PO.claim_nc = claim_nc;  // the open half replays the seal's log from the same first positions
+      PO.chain_in = (const uint2*)c->lpt_chain.p;
+    }
     if (rc == WG_OK && (gs != go || PS.slots != PO.slots || PS.order != PO.order))
       rc = fail(WG_EINVAL, "k_step: seal and open plans differ (%u / %u workgroups)", gs, go);
 #ifdef WG_DIAG
@@ -603,7 +634,8 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
     if (rc == WG_OK) {
       hipEvent_t ev;
       record_start(c, s, &ev);
-      if (PS.n_long) hipLaunchKernelGGL(wgt::k_step_mixed, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+      if (claim_nc) hipLaunchKernelGGL((wgt::k_step_claim<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+      else if (PS.n_long) hipLaunchKernelGGL(wgt::k_step_mixed, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else if (G == 16) hipLaunchKernelGGL(wgt::k_step<16>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else if (c->step_wpe4 && 2ull * gs * wgt::TW <= cap)
         hipLaunchKernelGGL((wgt::k_step<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
@@ -712,6 +744,7 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   if (const char* e = getenv("WG_UNIFORM16")) c->uniform16 = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_PRIO")) c->prio_mode = atoi(e);
   if (const char* e = getenv("WG_STEP_WPE4")) c->step_wpe4 = atoi(e) != 0;
+  if (const char* e = getenv("WG_CLAIM")) c->claim = atoi(e) != 0;
   if (const char* e = getenv("WG_TEST_STEP_FLIP")) {
     const long v = atol(e);
     c->test_flip = (v > 0 && (v & (v - 1)) == 0) ? (uint32_t)v : 0u;

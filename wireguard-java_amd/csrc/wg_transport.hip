@@ -122,6 +122,16 @@ struct TransportParams {
   const RxTables* rx;     // open with WG_F_RX_FILTER: receive-side verdict in the status (else NULL)
   const uint32_t* n_long; // k_*_mixed: device count of the packets at the front of the order that take
                           // 16-lane slots (written by k_lpt_scatter); NULL otherwise
+  // dynamic claims (k_step_claim, mixed-length batches): the longest-first order is dealt
+  // as claim_nc interleaved sub-orders (positions c, c + nc, c + 2 nc, ...), sub-order c to the workgroups
+  // b with b % nc == c; each slot starts on a static position and claims every later one from its
+  // sub-order's counter (claim[16 c], one 64-B line each, reset to claim_base by k_lpt_scatter), so a
+  // slot that finishes early takes the next-longest packet instead of a fixed one
+  uint32_t* claim;
+  uint32_t claim_nc;      // a power of two dividing the grid
+  uint32_t claim_base;    // slots per sub-order = the counters' initial value
+  uint2* chain_out;       // seal half of k_step_claim: per position {next position, next packet} of its slot
+  const uint2* chain_in;  // open half: the same chain, replayed (slot g opens exactly what it sealed)
   uint32_t test_flip;     // test hook (WG_TEST_STEP_FLIP=N, k_step only): N > 0 flips bit 0 of the sealed tag of
                           // each slot's first packet when its index is a multiple of N (a power of two); 0 in production
 #ifdef WG_DIAG
@@ -311,7 +321,12 @@ __device__ __forceinline__ uint32_t opaque_lane() {
 // 8 waves per SIMD).
 // iter: rounds this wave has run so far in the launch (the issue-priority schedule spans both
 // halves of a k_step launch).
-template <int MODE, int G = 8, bool VF = false>
+// Where a slot's packets come from (PM): kPosStatic, the snake over the grid (batch_pos); kPosClaim, a
+// static first position, then claims from the slot's sub-order counter, logged in P.chain_out when set;
+// kPosChain, the positions a kPosClaim seal half logged, in the same order.
+constexpr int kPosStatic = 0, kPosClaim = 1, kPosChain = 2;
+
+template <int MODE, int G = 8, bool VF = false, int PM = kPosStatic>
 __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_t blk, uint32_t wv, uint4* const img,
                                                SlotRec* const rec, uint32_t& iter) {
   static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
@@ -326,8 +341,18 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
   // descriptor prefetch: dword j of the next packet's wg_pkt (32 B = 8 dwords, one per lane)
   uint32_t gen = 0;
   uint32_t nxt;
+  // kPosClaim / kPosChain: the sub-order of this workgroup and the positions of the next / current packet
+  const uint32_t csub = PM != kPosStatic ? blk & (P.claim_nc - 1u) : 0u;
+  uint32_t npos = 0, cpos = 0;
   {
-    const uint32_t pos = batch_pos(g, 0, S);
+    uint32_t pos;
+    if constexpr (PM == kPosStatic) {
+      pos = batch_pos(g, 0, S);
+    } else {  // slot index inside the sub-order's workgroups, then the sub-order's position of it
+      const uint32_t gl = (blk / P.claim_nc) * (TW * (64u / G)) + (g - blk * TW * (64u / G));
+      pos = csub + P.claim_nc * gl;
+    }
+    npos = pos;
     nxt = pos < P.n ? (P.order ? P.order[pos] : pos) : ~0u;
   }
   uint32_t dnext = nxt != ~0u ? ((const uint32_t*)(P.desc + nxt))[opaque_lane() & 7u] : 0u;
@@ -409,8 +434,23 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
       have = true;
       // prefetch the descriptor of the slot's following packet
       ++gen;
-      const uint32_t pos = batch_pos(g, gen, S);
-      nxt = pos < P.n ? (P.order ? P.order[pos] : pos) : ~0u;
+      if constexpr (PM == kPosStatic) {
+        const uint32_t pos = batch_pos(g, gen, S);
+        nxt = pos < P.n ? (P.order ? P.order[pos] : pos) : ~0u;
+      } else if constexpr (PM == kPosClaim) {
+        cpos = npos;
+        uint32_t k = 0;
+        if (j == 0) k = atomicAdd(P.claim + 16u * csub, 1u);
+        const uint32_t pos = csub + P.claim_nc * bcastg<G, 0>(k);
+        nxt = pos < P.n ? (P.order ? P.order[pos] : pos) : ~0u;
+        npos = nxt != ~0u ? pos : ~0u;
+        if (P.chain_out && j == 0) P.chain_out[cpos] = make_uint2(npos, nxt);
+      } else {  // kPosChain
+        cpos = npos;
+        const uint2 cn = P.chain_in[cpos];  // every lane of the slot reads the same 8 B
+        npos = cn.x;
+        nxt = cn.y;
+      }
       dnext = nxt != ~0u ? ((const uint32_t*)(P.desc + nxt))[j & 7u] : 0u;
     }
     if (!__any(have)) break;
@@ -427,11 +467,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
       // (no registers held across the ARX rounds)
       const uint32_t lane = opaque_lane(), s = lane >> SH, j = lane & JM;
       const uint32_t b = G * round + j;
-#ifdef WG_ABL_NODMA
-      if (false) {
-#else
       if (have && b < nb && b > 0u) {
-#endif
         const uint32_t off = 64u * (b - 1u);
         const uint32_t nbytes = min(64u, len - off);
         const uint4 ad = rec[s].addr;
@@ -450,10 +486,6 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         }
       }
       // ---- ChaCha20: block b = 8 round + j ----------------------------------------------
-#ifdef WG_ABL_NOCHACHA  // ablation builds only (timing study; results are wrong)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) x[i] = b * 0x9e3779b9u + (uint32_t)i + meta.x;
-#else
       if (__any(have && round == 0)) {  // a new packet: its columns 1..3 of the first round, once
         const uint32_t c = j & 3u;
         const uint4* kl = rec[s].key;
@@ -473,7 +505,6 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
                                 bcastg<G, 3>(hc[0]), bcastg<G, 3>(hc[1]), bcastg<G, 3>(hc[2]), bcastg<G, 3>(hc[3])};
         chacha20_block_hoisted(rec[s].key, b, meta.x, meta.y, 0u, H, x);
       }
-#endif
     }
 
     const bool mac_pass = !VF || !(meta.w & kDecryptPass);  // the second pass of a verify-first open only decrypts
@@ -512,14 +543,10 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
             uint4 o = make_uint4(x[4 * q] ^ v.x, x[4 * q + 1] ^ v.y, x[4 * q + 2] ^ v.z, x[4 * q + 3] ^ v.w);
             if constexpr (MODE == WG_MODE_SEAL) {
               if (cb < 16u) o = mask_chunk(o, cb);
-#ifndef WG_ABL_NOMACW
               img[64u * q + lane] = o;  // the MAC input is the ciphertext
-#endif
             }
-#ifndef WG_ABL_NOSTORE
             if (!VF || (meta.w & (kVerifyFirst | kDecryptPass)) != kVerifyFirst)
               store_chunk(dst + 16u * q, cb, o, oal);
-#endif
           }
         }
       }
@@ -544,12 +571,8 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         const uint4 rr = rec[s].R0;
         uint32_t y[5];
         poly_r_limbs(rr.x, rr.y, rr.z, rr.w, y);
-#ifndef WG_ABL_NOSCAN
 #pragma unroll
         for (uint32_t st = 1; st < G; st <<= 1) {
-#else
-        for (uint32_t st = G; st < G; st <<= 1) {
-#endif
           uint32_t z[5], zs[5];
 #pragma unroll
           for (int i = 0; i < 5; ++i)
@@ -585,11 +608,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
 
     WG_PH(3);
     // ---- Poly1305 over this round's chunks -------------------------------------------------
-#ifdef WG_ABL_NOPOLY
-    if (false) {
-#else
     if (have && (meta.w & 1u) && mac_pass) {
-#endif
       const uint32_t lane = opaque_lane(), s = lane >> SH, j = lane & JM;
       {
         const uint32_t nc = (len + 15u) >> 4;
@@ -644,11 +663,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
 #pragma unroll
         for (uint32_t t = 0; t < 4u; ++t) {
           if (c0 + G * t < c_end) {
-#ifndef WG_ABL_NOPOLYLDS
             uint4 v = ip[(G / 4u) * t];
-#else
-            uint4 v = make_uint4(acc[0] ^ t, acc[1], acc[2] + c0, acc[3]);
-#endif
             // acc is still 0 before a packet's first chunk (round 0, t = 0): no product needed
             if (round != 0 || t != 0) poly_mul(acc, R, Rs);
             uint32_t cl[5];
@@ -684,11 +699,9 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
               acc[3] += len >> 14;
               acc[4] += 1u << 24;
             }
-#ifndef WG_ABL_NOFINISH
             uint32_t Ws[5];
             poly_scale5(W, Ws);
             poly_mul(acc, W, Ws);
-#endif
           }
 #pragma unroll
           for (int i = 0; i < 5; ++i) {  // slot sum (every lane of the slot ends with it)
@@ -706,11 +719,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         if (mac_pass && valid && j == 0) {
           const uint4 sv = rec[s].s;
           uint32_t tag[4];
-#ifndef WG_ABL_NOFINISH
           poly_finish(acc, sv.x, sv.y, sv.z, sv.w, tag);
-#else
-          tag[0] = acc[0] ^ sv.x; tag[1] = acc[1] ^ sv.y; tag[2] = acc[2] ^ sv.z; tag[3] = acc[3] ^ sv.w;
-#endif
           if constexpr (MODE == WG_MODE_SEAL) {
             uint8_t* tp = outp + len;
             if ((((uintptr_t)tp) & 15u) == 0) {
@@ -900,6 +909,21 @@ k_step(TransportParams S, TransportParams O) {
   transport_body<WG_MODE_OPEN, G>(O, blockIdx.x, wv, img_[wv], rec_[wv], iter);
 }
 
+// k_step with dynamic claims (mixed-length batches, WG_CLAIM): the seal half claims its slots' packets
+// from the sub-order counters and logs them per position; the open half replays that log, so slot g
+// opens exactly what it sealed (the same wave wrote it: the half boundary below orders the accesses).
+template <int G = 8, int WPE = 4>
+__global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(WPE)))
+k_step_claim(TransportParams S, TransportParams O) {
+  __shared__ uint4 img_[TW][4 * 64];
+  __shared__ SlotRec rec_[TW][8];
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t iter = 0;
+  transport_body<WG_MODE_SEAL, G, false, kPosClaim>(S, blockIdx.x, wv, img_[wv], rec_[wv], iter);
+  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
+  transport_body<WG_MODE_OPEN, G, false, kPosChain>(O, blockIdx.x, wv, img_[wv], rec_[wv], iter);
+}
+
 // ---- longest-first order for mixed-length batches (LPT) ----------------------------------
 // key = rounds of the packet (invalid lengths sort last); counting sort into descending keys.
 template <int MODE>
@@ -939,7 +963,10 @@ __global__ void __launch_bounds__(LPT_THREADS) k_lpt_hist(const wg_pkt* d, uint3
 template <int MODE>
 __global__ void __launch_bounds__(LPT_THREADS) k_lpt_scatter(const wg_pkt* d, uint32_t n, uint32_t max_len,
                                                              const uint32_t* bh, uint32_t* order, uint32_t split,
-                                                             uint32_t* n_long) {
+                                                             uint32_t* n_long, uint32_t* claim, uint32_t claim_nc,
+                                                             uint32_t claim_base) {
+  // the dynamic-claim counters of the launch this order is for (k_step_claim): one 64-B line each
+  if (claim && blockIdx.x == 0 && threadIdx.x < claim_nc) claim[16u * threadIdx.x] = claim_base;
   __shared__ uint32_t all[LPT_MAX_BLOCKS * LPT_BINS];  // every block's histogram (coalesced load)
   __shared__ uint32_t tot[LPT_BINS], base[LPT_BINS];
   for (uint32_t e = threadIdx.x; e < gridDim.x * LPT_BINS; e += LPT_THREADS) all[e] = bh[e];
