@@ -251,14 +251,20 @@ def test_held_caller_delays_nobody():
     descheduled mid-call, test hook WG_PP_TEST_HOLD_*) while 16 others run: with out-of-order
     service nobody waits for it (the round-3 in-order ticket server stalled every later ticket of
     its wave for the whole 50 ms)."""
-    j = _batcher_bench(16, 2000, 1420, "hold_us=50000")
+    j = _batcher_bench(16, 2000, 1420, "hold_us=50000", "stamps=1")
     print(j)
     assert j["failures"] == 0 and j["held_rc"] == 0
     assert j["held_us"] >= 50000
     assert j["lat_us"]["p999"] < 2000, j["lat_us"]
-    # the single slowest of the 32,000 calls: 0.05-3.5 ms on the boxes so far (one outlier per run at
-    # most; DESIGN.md §9), far below the 50 ms that waiting for the held entry would add
-    assert j["lat_us"]["max"] < 20000, (j["lat_us"], j["throttled_periods"])
+    # The single slowest of the 32,000 calls, with its stages (wg_pp_last_call) and the caller thread's
+    # context switches: the device served it in its usual ~8 us, and it stayed under 2 ms unless the OS
+    # preempted the calling thread during it (an involuntary context switch: round 5 traced every
+    # 0.2-ms outlier of six runs to one, DESIGN.md §9) or the cgroup quota throttled the process.
+    # Waiting for the held entry would add 50 ms.
+    slow = j["slowest"]
+    assert slow["device_service_us"] < 100, slow
+    preempted = slow["involuntary_csw"] > 0 or j["throttled_periods"] > 0
+    assert j["lat_us"]["max"] < (20000 if preempted else 2000), (j["lat_us"], slow, j["throttled_periods"])
 
 
 @pytest.mark.gpu
