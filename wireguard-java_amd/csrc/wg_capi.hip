@@ -620,7 +620,6 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
                                         c->lpt_order, &PO, &go, &oo, nullptr, true, true, sp.split);
     // one issue-priority schedule over the seal and open halves (the rounds of both)
     if (PS.prio_step) PS.prio_step = PO.prio_step = 2u * PS.prio_step;
-    PS.test_flip = c->test_flip;
     if (claim_nc) {
       PS.chain_out = (uint2*)c->lpt_chain.p;
       PO.claim_nc = claim_nc;  // the open half replays the seal's log from the same first positions
@@ -636,10 +635,12 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
       record_start(c, s, &ev);
       if (claim_nc) hipLaunchKernelGGL((wgt::k_step_claim<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else if (PS.n_long) hipLaunchKernelGGL(wgt::k_step_mixed, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
-      else if (G == 16) hipLaunchKernelGGL(wgt::k_step<16>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+      else if (c->test_flip && G == 8)  // test hook build: the same body with the tag flip between the halves
+        hipLaunchKernelGGL((wgt::k_step<8, 4, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, c->test_flip);
+      else if (G == 16) hipLaunchKernelGGL(wgt::k_step<16>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
       else if (c->step_wpe4 && 2ull * gs * wgt::TW <= cap)
-        hipLaunchKernelGGL((wgt::k_step<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
-      else hipLaunchKernelGGL(wgt::k_step<8>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+        hipLaunchKernelGGL((wgt::k_step<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
+      else hipLaunchKernelGGL(wgt::k_step<8>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
       const hipError_t e = hipGetLastError();
       record_end(c, s, ev);
       if (e != hipSuccess) rc = fail(WG_EDEVICE, "k_step launch: %s", hipGetErrorString(e));

@@ -132,8 +132,6 @@ struct TransportParams {
   uint32_t claim_base;    // slots per sub-order = the counters' initial value
   uint2* chain_out;       // seal half of k_step_claim: per position {next position, next packet} of its slot
   const uint2* chain_in;  // open half: the same chain, replayed (slot g opens exactly what it sealed)
-  uint32_t test_flip;     // test hook (WG_TEST_STEP_FLIP=N, k_step only): N > 0 flips bit 0 of the sealed tag of
-                          // each slot's first packet when its index is a multiple of N (a power of two); 0 in production
 #ifdef WG_DIAG
   uint64_t* stamps;       // diagnostic build only: 10 x u64 per wave (cycles per phase, start/end times)
 #endif
@@ -881,12 +879,12 @@ k_duplex(TransportParams S, TransportParams O, uint32_t seal_blocks, uint32_t op
 // differs from the reference, so the bench's check of the k_step output it timed must fail
 // (tests/test_gpu_bench.py). Outside transport_body: the product body's code is unchanged.
 template <int G>
-__device__ __forceinline__ void step_test_flip(const TransportParams& S, uint32_t blk, uint32_t wv) {
+__device__ __forceinline__ void step_test_flip(const TransportParams& S, uint32_t blk, uint32_t wv, uint32_t flip) {
   const uint32_t lane = threadIdx.x & 63u, g = (blk * TW + wv) * (64u / G) + lane / G;
   if ((lane & (G - 1u)) == 0u && g < S.n) {
     const uint32_t i = S.order ? S.order[g] : g;
     const wg_pkt d = S.desc[i];
-    if ((i & (S.test_flip - 1u)) == 0u &&
+    if ((i & (flip - 1u)) == 0u &&
         transport_valid<WG_MODE_SEAL>(d.in_off, d.out_off, d.len, d.key_slot, S.max_len, S.key_slots, S.in_size,
                                       S.out_size))
       S.out[d.out_off + d.len] ^= 1u;
@@ -894,9 +892,10 @@ __device__ __forceinline__ void step_test_flip(const TransportParams& S, uint32_
   asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
 }
 
-template <int G = 8, int WPE = 8>
+// FLIP: the test-hook build (WG_TEST_STEP_FLIP); the product instantiations carry no hook code at all.
+template <int G = 8, int WPE = 8, bool FLIP = false>
 __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(WPE)))
-k_step(TransportParams S, TransportParams O) {
+k_step(TransportParams S, TransportParams O, uint32_t test_flip) {
   __shared__ uint4 img_[TW][4 * 64];
   __shared__ SlotRec rec_[TW][8];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -905,7 +904,7 @@ k_step(TransportParams S, TransportParams O) {
   // the open reads the ciphertext and tags this wave just stored: wait until the stores are
   // performed and drop this CU's L1 lines (an in-place seal read the plaintext through them)
   asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
-  if (S.test_flip) step_test_flip<G>(S, blockIdx.x, wv);
+  if constexpr (FLIP) step_test_flip<G>(S, blockIdx.x, wv, test_flip);
   transport_body<WG_MODE_OPEN, G>(O, blockIdx.x, wv, img_[wv], rec_[wv], iter);
 }
 
