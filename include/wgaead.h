@@ -340,7 +340,8 @@ int wg_open1(wg_ctx* ctx, uint32_t key_slot, uint64_t counter, const uint8_t* in
 int wg_pp_config(wg_ctx* ctx, uint32_t waves, uint32_t idle_us);
 /* Diagnostic: the stages of the calling thread's last wg_seal1 / wg_open1, in ns (out[0..7]: total,
  * claim, publish, wait for the completion, device service time, copy-out, slept on the futex 0/1,
- * relaunched the server 0/1); tools/batcher_bench stamps=1 reports the slowest call's. */
+ * relaunched the server 0/1); recorded only when WG_PP_CALL_STAMPS=1 is set before the context's
+ * first per-packet call (zeros otherwise); tools/batcher_bench stamps=1 reports the slowest call's. */
 int wg_pp_last_call(uint64_t* out, uint32_t n);
 int wg_batcher_config(wg_ctx* ctx, uint32_t max_batch, uint32_t window_us);
 int wg_batcher_stats(wg_ctx* ctx, uint64_t* launches, uint64_t* packets);

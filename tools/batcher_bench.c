@@ -170,6 +170,7 @@ int main(int argc, char** argv) {
     snprintf(buf, sizeof buf, "%d", hold_us);
     setenv("WG_PP_TEST_HOLD_US", buf, 1);
   }
+  if (g_stamps) setenv("WG_PP_CALL_STAMPS", "1", 1);
   if (fail_launches) {
     snprintf(buf, sizeof buf, "%d", fail_launches);
     setenv("WG_PP_TEST_FAIL_LAUNCHES", buf, 1);

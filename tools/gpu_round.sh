@@ -25,6 +25,9 @@ tail -1 $O/smoke.log
 step "bench c1 (step)"
 timeout -k 10 400 python bench.py > $O/bench_c1.json 2> $O/bench.err || die bench_c1 $?
 cat $O/bench_c1.json
+timeout -k 10 400 python bench.py > $O/bench_c1b.json 2>> $O/bench.err || die bench_c1b $?
+step "bench c1 under torchrun (RCCL group of one rank)"
+timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 1 > $O/bench_c1_torchrun1.json 2>> $O/bench.err || die bench_c1_torchrun $?
 step "bench c1 (serial)"
 timeout -k 10 300 python bench.py --mode serial --no-cpu-baseline > $O/bench_c1_serial.json 2>> $O/bench.err || die bench_c1_serial $?
 step "bench c1 (step as two launches)"
@@ -56,15 +59,19 @@ timeout -k 10 120 ./tools/pp_stamps 1420 > $O/pp_stamps.json || die pp_stamps $?
 fi
 [ "$PART" = bench ] && { step done; exit 0; }
 cd /tmp && export TMPDIR=/tmp
-for w in c1 c2; do
+# c1s: C1 with one stream per step (--streams 1): the launch the line's roofline (kernel_ms, frac, traffic)
+# describes; c1: the default two-stream step (the line's value); c2: one stream by default
+for w in c1s c1 c2; do
+  wl=${w%s}; xs=""; [ $w = c1s ] && xs="--streams 1"
   step "rocprofv3 kernel trace $w"
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_$w -o run --output-format csv -- python3 $ROOT/bench.py --workload $w --no-cpu-baseline > $O/prof_bench_$w.json 2> $O/prof_$w.log || die prof_$w $?
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_$w -o run --output-format csv -- python3 $ROOT/bench.py --workload $wl $xs --no-cpu-baseline > $O/prof_bench_$w.json 2> $O/prof_$w.log || die prof_$w $?
   python3 $ROOT/tools/prof_window.py trace $(find $O/prof_$w -name "run_kernel_trace.csv" | head -1) $O/prof_bench_$w.json --out $O/window_$w.json > /dev/null || die window_$w $?
+  [ $w = c1 ] && continue  # counters: the one-stream launches (c1s) and C2
   i=0
   for grp in FETCH_SIZE WRITE_SIZE "SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE"; do
     i=$((i+1))
     step "pmc $w $grp"
-    timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d $O/pmc/${w}_p$i -o run --output-format csv -- python3 $ROOT/bench.py --workload $w --no-cpu-baseline --steps 20 --warmup 2 > $O/pmc/${w}_p$i.json 2> $O/pmc/${w}_p$i.log || die pmc_${w}_$i $?
+    timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d $O/pmc/${w}_p$i -o run --output-format csv -- python3 $ROOT/bench.py --workload $wl $xs --no-cpu-baseline --steps 20 --warmup 2 > $O/pmc/${w}_p$i.json 2> $O/pmc/${w}_p$i.log || die pmc_${w}_$i $?
   done
   args=""
   for j in 1 2 3 4; do args="$args $(find $O/pmc/${w}_p$j -name '*counter_collection.csv' | head -1) $O/pmc/${w}_p$j.json"; done

@@ -7,7 +7,10 @@
  *
  * Build: make -C tools queue_bench
  * Run:   tools/queue_bench [producers=16] [packets_per_producer=200000] [len=1420|0 mixed 64..1500]
- *                          [max_batch=8192] [forwarders=1] [verifiers=1]
+ *                          [max_batch=8192] [forwarders=1] [verifiers=1] [cpu_port=PATH]
+ * cpu_port=oracle/liboracle.so: after the queue run, the CPU restatement of the reference's AEAD seals
+ * and opens the SAME packets (lengths, keys, counters) on `producers` threads, in the same process and
+ * run, so the line compares the queue with the CPU port on exactly this packet mix ("cpu_port_gib_s").
  * Output: one JSON line: seal+open payload GiB/s over the whole run (both directions' payload bytes,
  * as bench.py's cpu_baseline counts them), seal-side rate, latency percentiles per queue (submit ->
  * reap), batches per queue. Exit status 1 on any failed status or byte mismatch. */
@@ -21,6 +24,7 @@
 #include <string.h>
 #include <sys/resource.h>
 #include <time.h>
+#include <dlfcn.h>
 
 #include "wgaead.h"
 
@@ -198,6 +202,9 @@ int main(int argc, char** argv) {
   g_len = argc > 3 ? atoi(argv[3]) : 1420;
   const int max_batch = argc > 4 ? atoi(argv[4]) : 8192;
   const int nf = argc > 5 ? atoi(argv[5]) : 1, nv = argc > 6 ? atoi(argv[6]) : 1;
+  const char* cpu_port = NULL;
+  for (int a = 1; a < argc; ++a)
+    if (!strncmp(argv[a], "cpu_port=", 9)) cpu_port = argv[a] + 9;
   if (g_P < 1 || g_P > 256 || g_N < 1 || g_len < 0 || g_len > 1500) {
     fprintf(stderr, "usage: queue_bench [producers] [packets_per_producer] [len 0..1500] [max_batch]\n");
     return 2;
@@ -269,20 +276,62 @@ int main(int argc, char** argv) {
   pct(g_lat_s, ns, ls);
   pct(g_lat_o, no, lo);
   const double gib = (double)(1u << 30);
+  /* the CPU port on the same packets: seal every packet, then open every ct || tag, producers threads */
+  double cpu_port_gib_s = 0, cpu_port_s = 0;
+  int cpu_port_ok = 1;
+  if (cpu_port) {
+    void* h = dlopen(cpu_port, RTLD_NOW);
+    int (*o_seal)(const wg_pkt*, size_t, const uint8_t*, uint8_t*, const uint8_t*, int) =
+        h ? (int (*)(const wg_pkt*, size_t, const uint8_t*, uint8_t*, const uint8_t*, int))dlsym(h, "oracle_seal_batch") : NULL;
+    int (*o_open)(const wg_pkt*, size_t, const uint8_t*, uint8_t*, const uint8_t*, uint32_t*, int) =
+        h ? (int (*)(const wg_pkt*, size_t, const uint8_t*, uint8_t*, const uint8_t*, uint32_t*, int))dlsym(h, "oracle_open_batch") : NULL;
+    if (!o_seal || !o_open) {
+      fprintf(stderr, "cpu_port=%s: %s\n", cpu_port, dlerror());
+      return 1;
+    }
+    /* a bounded sample of the same packets (at most 1M): user ids t << 40 | i, round robin over producers */
+    const uint64_t n = g_total < (1u << 20) ? g_total : (1u << 20);
+    wg_pkt* sd = calloc(n, sizeof(wg_pkt));
+    wg_pkt* od = calloc(n, sizeof(wg_pkt));
+    uint32_t* st = calloc(n, sizeof(uint32_t));
+    uint64_t off = 0, cbytes = 0;
+    for (uint64_t k = 0; k < n; ++k) {
+      const uint64_t user = ((k % (uint64_t)g_P) << 40) | (k / (uint64_t)g_P);
+      const uint32_t L = pkt_len(user);
+      sd[k] = (wg_pkt){off, off, k / (uint64_t)g_P, L, (uint32_t)(k % (uint64_t)g_P) % KEYS};
+      off += ((uint64_t)L + 16u + 15u) & ~15ull;
+      cbytes += L;
+    }
+    uint8_t* pt = malloc(off), *ct = malloc(off), *back = malloc(off);
+    for (uint64_t k = 0; k < n; ++k) fill(pt + sd[k].in_off, ((k % (uint64_t)g_P) << 40) | (k / (uint64_t)g_P), sd[k].len);
+    memcpy(od, sd, n * sizeof(wg_pkt));
+    const uint64_t c0 = now_ns();
+    o_seal(sd, n, pt, ct, keys, g_P);
+    o_open(od, n, ct, back, keys, st, g_P);
+    cpu_port_s = (now_ns() - c0) * 1e-9;
+    for (uint64_t k = 0; k < n; ++k)
+      if (st[k] != WG_PKT_OK || memcmp(back + sd[k].in_off, pt + sd[k].in_off, sd[k].len) != 0) cpu_port_ok = 0;
+    cpu_port_gib_s = 2.0 * cbytes / cpu_port_s / gib;
+    free(sd); free(od); free(st); free(pt); free(ct); free(back);
+  }
+  char cpu_json[256] = "";
+  if (cpu_port)
+    snprintf(cpu_json, sizeof cpu_json, ", \"cpu_port_gib_s\": %.3f, \"cpu_port_threads\": %d, \"cpu_port_ok\": %d",
+             cpu_port_gib_s, g_P, cpu_port_ok);
   printf("{\"tool\": \"queue_bench\", \"producers\": %d, \"forwarders\": %d, \"verifiers\": %d, \"packets\": %llu, \"len\": \"%s\", \"max_batch\": %d, "
          "\"bad\": %llu, \"wall_s\": %.4f, \"seal_open_gib_s\": %.3f, \"seal_gib_s\": %.3f, "
          "\"submit_gib_s\": %.3f, \"packets_per_s\": %.0f, "
          "\"seal_lat_us\": {\"p50\": %.1f, \"p99\": %.1f, \"p999\": %.1f, \"max\": %.1f}, "
          "\"open_lat_us\": {\"p50\": %.1f, \"p99\": %.1f, \"p999\": %.1f, \"max\": %.1f}, "
          "\"seal_batches\": %llu, \"seal_mean_batch\": %.1f, \"open_batches\": %llu, \"open_mean_batch\": %.1f, "
-         "\"cpu_s\": %.3f, \"cpus_busy\": %.2f, \"throttled_periods\": %llu, \"throttled_ms\": %.1f, \"pinned_node\": %d}\n",
+         "\"cpu_s\": %.3f, \"cpus_busy\": %.2f, \"throttled_periods\": %llu, \"throttled_ms\": %.1f, \"pinned_node\": %d%s}\n",
          g_P, nf, nv, (unsigned long long)g_total, g_len ? argv[3] : "mixed 64..1500", max_batch,
          (unsigned long long)g_bad, wall, 2.0 * bytes / wall / gib, bytes / t_sealed / gib, bytes / t_submit / gib,
          g_total / wall, ls[0], ls[1], ls[2], ls[3], lo[0], lo[1], lo[2], lo[3], (unsigned long long)bs,
          bs ? (double)ps / bs : 0.0, (unsigned long long)bo, bo ? (double)po / bo : 0.0, cpu, cpu / wall,
-         thp1 - thp0, (thu1 - thu0) * 1e-3, pinned);
+         thp1 - thp0, (thu1 - thu0) * 1e-3, pinned, cpu_json);
   wg_queue_destroy(g_qs);
   wg_queue_destroy(g_qo);
   wg_ctx_destroy(g_ctx);
-  return g_bad ? 1 : 0;
+  return (g_bad || !cpu_port_ok) ? 1 : 0;
 }

@@ -245,8 +245,10 @@ __device__ void pp_packet(const Hdr& h, uint64_t ticket, const uint8_t* slot, ui
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every result byte has landed before done
   PP_STAMP(ticket, 6);
   if (lane == 0) {
-    // the service time first: it is ordered before the completion word the caller polls for
-    __hip_atomic_store(svc, __builtin_amdgcn_s_memrealtime() - t_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // the service time first (only with WG_PP_CALL_STAMPS: one more PCIe write per packet): it is
+    // ordered before the completion word the caller polls for
+    if (svc)
+      __hip_atomic_store(svc, __builtin_amdgcn_s_memrealtime() - t_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(done, (ticket << 8) | status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
@@ -323,7 +325,8 @@ __global__ void __launch_bounds__(64) k_pp(PPParams P) {
 #endif
           PP_STAMP(seq, 1);
           if (h.len <= kPPMaxLen && (h.mode == WG_MODE_SEAL || h.mode == WG_MODE_OPEN)) {
-            pp_packet(h, seq, slot, P.out + (size_t)i * kOutSlot, P.done + i, img_in, img_out, P.svc + i, t_seen);
+            pp_packet(h, seq, slot, P.out + (size_t)i * kOutSlot, P.done + i, img_in, img_out, P.svc ? P.svc + i : nullptr,
+                      t_seen);
           } else if (lane == 0) {  // refused by the host before publishing; never expected here
             __hip_atomic_store(P.done + i, (seq << 8) | 0xffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           }
@@ -421,6 +424,7 @@ struct PPServer {
   std::atomic<bool> waker_quit{false};
   std::mutex wmu;
   std::condition_variable wcv;
+  bool stamps = false;            // WG_PP_CALL_STAMPS=1: per-call stage stamps (wg_pp_last_call), off by default
   uint64_t hold_counter = ~0ull;  // test hook (WG_PP_TEST_HOLD_COUNTER / _US): a call with this counter
   uint32_t hold_us = 0;           // sleeps between claiming its entry and publishing it
 
@@ -468,6 +472,7 @@ int pp_get(wg_ctx* c, PPServer** out) {
   if (const char* e = getenv("WG_PP_TEST_HOLD_COUNTER")) S->hold_counter = strtoull(e, nullptr, 0);
   if (const char* e = getenv("WG_PP_TEST_HOLD_US")) S->hold_us = (uint32_t)atoi(e);
   if (const char* e = getenv("WG_PP_SPIN")) S->spin_limit = (uint32_t)std::max(1, atoi(e));
+  if (const char* e = getenv("WG_PP_CALL_STAMPS")) S->stamps = atoi(e) != 0;
   S->spin_callers = host_cpus();
   if (const char* e = getenv("WG_PP_SPIN_CALLERS")) S->spin_callers = (uint32_t)std::max(0, atoi(e));
   S->wake.reset(new std::atomic<uint32_t>[wgpp::kRing]);
@@ -511,7 +516,7 @@ int pp_ensure(PPServer* S) {
   P.bell = (const uint64_t*)(S->dev + S->bell_off());
   P.ctl = (const wgpp::Ctl*)(S->dev + S->ctl_off());
   P.exit_flag = (uint64_t*)(S->dev + S->exit_off());
-  P.svc = (uint64_t*)(S->dev + S->svc_off());
+  P.svc = S->stamps ? (uint64_t*)(S->dev + S->svc_off()) : nullptr;
   P.ack = S->d_ack;
   P.exited = S->d_exited;
   P.quit = S->d_exited + 1;
@@ -692,18 +697,21 @@ int pp_sleep(PPServer* S, uint32_t i, uint64_t seq, uint64_t* d_out) {
 int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const uint8_t* src, uint32_t len,
               uint8_t* dst) {
   if (len > wgpp::kPPMaxLen) return pp_big(c, open, key_slot, counter, src, len, dst);
-  PPCallStamps& st = g_pp_last;
-  st = PPCallStamps{};
-  st.t_enter = pp_now_ns();
   PPServer* S;
   int rc;
   if ((rc = pp_get(c, &S)) != WG_OK) return rc;
+  // per-call stage stamps only with WG_PP_CALL_STAMPS (a stamped call writes into a dummy otherwise)
+  PPCallStamps dummy;
+  PPCallStamps& st = S->stamps ? g_pp_last : dummy;
+  const bool stamp = S->stamps;
+  st = PPCallStamps{};
+  if (stamp) st.t_enter = pp_now_ns();
   uint32_t key[8];
   key_snapshot(c, key_slot, key);
   const uint64_t k = S->calls.fetch_add(1, std::memory_order_relaxed);
   const uint64_t seq = k + 1;  // unique per call: the completion word echoes it
   const uint32_t i = pp_claim(S, k);
-  st.t_claimed = pp_now_ns();
+  if (stamp) st.t_claimed = pp_now_ns();
   const uint64_t launches0 = S->launches.load(std::memory_order_relaxed);
   wgpp::Hdr* h = (wgpp::Hdr*)S->in_slot(i);
   h->seq = seq;
@@ -719,7 +727,7 @@ int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const u
   // publish: toggle the entry's doorbell bit (a locked RMW, ordered after every byte above)
   __atomic_fetch_xor(S->bell(i >> 6), 1ull << (i & 63u), __ATOMIC_SEQ_CST);
   rc = pp_ensure(S);
-  st.t_published = pp_now_ns();
+  if (stamp) st.t_published = pp_now_ns();
   uint64_t d = 0;
   // with more calls in flight than spin_callers, a caller that polls for its whole round trip burns a
   // core the host does not have (and under a CPU quota every thread of the process then stalls until
@@ -738,11 +746,13 @@ int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const u
     __builtin_ia32_pause();
   }
   S->active.fetch_sub(1, std::memory_order_relaxed);
-  st.t_complete = pp_now_ns();
-  st.relaunched = S->launches.load(std::memory_order_relaxed) != launches0 ? 1u : 0u;
+  if (stamp) {
+    st.t_complete = pp_now_ns();
+    st.relaunched = S->launches.load(std::memory_order_relaxed) != launches0 ? 1u : 0u;
+  }
   int result = rc;
   if (rc == WG_OK) {
-    st.svc_ticks = *S->svc(i);
+    if (stamp) st.svc_ticks = *S->svc(i);
     const uint32_t status = (uint32_t)(d & 0xffu);
     if (status == WG_PKT_OK) {
       if (open) {
@@ -762,7 +772,7 @@ int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const u
     // completion word has landed, so the entry is never lost
     S->state[i].store(kOrphan, std::memory_order_release);
   }
-  st.t_exit = pp_now_ns();
+  if (stamp) st.t_exit = pp_now_ns();
   return result;
 }
 

@@ -79,6 +79,33 @@ struct IdQueue {
       }
     }
   }
+  // Up to max ids at once: one CAS on head for the whole run of ready cells (a consumer popping a
+  // burst of completions claims them together instead of one CAS per id). Returns how many.
+  uint32_t pop_n(uint32_t* v, uint32_t max) {
+    uint64_t pos = head.load(std::memory_order_relaxed);
+    for (;;) {
+      uint32_t k = 0;
+      while (k < max) {
+        const uint64_t seq = buf[(pos + k) & mask].seq.load(std::memory_order_acquire);
+        if ((int64_t)seq - (int64_t)(pos + k + 1) != 0) break;
+        ++k;
+      }
+      if (k == 0) {
+        const uint64_t h = head.load(std::memory_order_relaxed);
+        if (h == pos) return 0;  // empty
+        pos = h;
+        continue;
+      }
+      if (head.compare_exchange_weak(pos, pos + k, std::memory_order_relaxed)) {
+        for (uint32_t i = 0; i < k; ++i) {
+          Cell& c = buf[(pos + i) & mask];
+          v[i] = c.v;
+          c.seq.store(pos + i + mask + 1, std::memory_order_release);
+        }
+        return k;
+      }
+    }
+  }
   uint64_t size_hint() const {
     const uint64_t t = tail.load(std::memory_order_relaxed), h = head.load(std::memory_order_relaxed);
     return t > h ? t - h : 0;
@@ -192,7 +219,6 @@ struct wg_queue {
   wgq::IdQueue done_q;                // completions: pushed by the dispatcher, popped by consumers
   uint32_t lanes = 0, per_lane = 0;     // producer lanes and the ring slots each owns
   std::unique_ptr<wgq::Lane[]> lane;
-  std::atomic<uint64_t> ready_hint{0};  // submissions not yet taken by the dispatcher (its sleep test)
   // producers that found no free slot sleep on `wake_word` until wg_reap_done has handed back
   // wake_batch slots since the last wake (not one wake per freed slot: 16 producers woken for every
   // reap burn the CPU the consumer needs to free slots, and fill the ring one packet at a time)
@@ -252,6 +278,14 @@ void queue_complete(wg_queue* q, wgq::Batch& b, uint32_t status_override) {
   }
 }
 
+// Any lane with a submitted packet the dispatcher has not gathered yet (its sleep test).
+bool queue_any_ready(wg_queue* q) {
+  for (uint32_t l = 0; l < q->lanes; ++l)
+    if (q->lane[l].r_tail.load(std::memory_order_acquire) != q->lane[l].r_head.load(std::memory_order_relaxed))
+      return true;
+  return false;
+}
+
 void queue_dispatch(wg_queue* q) {
   DeviceGuard g(q->c->device);
   // short naps below (a few us) must not be stretched to the default 50-us timer slack
@@ -300,10 +334,7 @@ void queue_dispatch(wg_queue* q) {
         ln.r_head.store(h, std::memory_order_relaxed);
       }
       rr = (rr + 1) % q->lanes;
-      if (taken) {
-        q->ready_hint.fetch_sub(taken, std::memory_order_relaxed);
-        idle = 0;
-      }
+      if (taken) idle = 0;
       // launch once min_batch packets wait, or when the first of them has waited window_ns (a light
       // load: one packet waits at most that long; a heavy one fills batches of min_batch and more)
       if (fill->n > 0 && (fill->n >= q->min_batch || wgq::now_ns() - first_ns >= q->window_ns)) {
@@ -331,8 +362,11 @@ void queue_dispatch(wg_queue* q) {
     }
     // nothing in flight and nothing ready: sleep until a producer pushes (or 1 ms)
     std::unique_lock<std::mutex> lk(q->mu);
+    // Dekker with queue_submit: idle flag, full fence, then the lanes; a producer publishes, fences and
+    // then reads the flag, so either this scan sees its packet or it sees the flag and notifies
     q->disp_idle.store(1, std::memory_order_seq_cst);
-    if (q->ready_hint.load() == 0 && !q->quit.load())
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    if (!queue_any_ready(q) && !q->quit.load())
       q->cv_disp.wait_for(lk, std::chrono::milliseconds(1));
     q->disp_idle.store(0, std::memory_order_relaxed);
   }
@@ -460,8 +494,9 @@ int queue_submit(wg_queue* q, int mode, uint32_t key_slot, uint64_t counter, con
   ln.ready[rt % q->per_lane] = s;
   ln.r_tail.store(rt + 1, std::memory_order_release);  // publish: after the slot's bytes and meta
   wgq::spin_unlock(ln.lock);
-  q->ready_hint.fetch_add(1, std::memory_order_relaxed);
-  if (q->disp_idle.load(std::memory_order_seq_cst)) {
+  // (no shared per-packet counter: 16 producers incrementing one cache line per packet serialised on it)
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  if (q->disp_idle.load(std::memory_order_relaxed)) {
     std::lock_guard<std::mutex> lk(q->mu);
     q->cv_disp.notify_one();
   }
@@ -603,7 +638,11 @@ int wg_reap(wg_queue* q, wg_completion* out, uint32_t max, uint32_t timeout_us) 
   uint32_t n = 0, s;
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us);
   while (true) {
-    while (n < max && q->done_q.pop(&s)) {
+    uint32_t ids[256];
+    uint32_t got;
+    while (n < max && (got = q->done_q.pop_n(ids, std::min<uint32_t>(256u, max - n))) > 0) {
+     for (uint32_t k = 0; k < got; ++k) {
+      s = ids[k];
       const wgq::SlotMeta& m = q->meta[s];
       wg_completion& o = out[n++];
       o.user = m.user;
@@ -614,6 +653,7 @@ int wg_reap(wg_queue* q, wg_completion* out, uint32_t max, uint32_t timeout_us) 
       o.key_slot = m.key_slot;
       o.slot = s;
       o.submit_ns = m.t_submit_ns;
+     }
     }
     if (n > 0 || timeout_us == 0 || max == 0) return (int)n;
     if (const int e = q->err.load(std::memory_order_relaxed)) return fail(e, "queue failed");
