@@ -397,10 +397,13 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   const uint32_t waves = (uint32_t)((n + spw * per_slot - 1) / (spw * per_slot));
   const uint32_t grid = mixed ? (n + 4u * wgt::TW - 1u) / (4u * wgt::TW) + 2u : (waves + wgt::TW - 1) / wgt::TW;
   P.slots = grid * wgt::TW * spw;
-  if (claim) {
+  if (claim) {  // k_step_claim: the largest power of two <= claim_nc that divides the grid (every sub-order
+                // then has the same number of workgroups, and its static first positions end at claim_base)
+    uint32_t nc = claim_nc;
+    while (nc > 1 && grid % nc) nc >>= 1;
     P.claim = claim;
-    P.claim_nc = claim_nc;
-    P.claim_base = P.slots / claim_nc;
+    P.claim_nc = nc;
+    P.claim_base = P.slots / nc;
   }
   // mixed lengths: the rounds a slot runs, spread over the 4 issue-priority levels (k_transport),
   // so the waves that have done the least work issue first (C2 +2%); uniform batches keep the
@@ -425,7 +428,7 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
       hipLaunchKernelGGL((wgt::k_lpt_hist<MODE>), dim3(lgrid), dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len, bh);
       hipLaunchKernelGGL((wgt::k_lpt_scatter<MODE>), dim3(lgrid), dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len,
                          (const uint32_t*)bh, (uint32_t*)lpt_order.p, split,
-                         mixed ? (uint32_t*)c->lpt_nlong.p : nullptr, claim, claim_nc, P.claim_base);
+                         mixed ? (uint32_t*)c->lpt_nlong.p : nullptr, claim, P.claim_nc, P.claim_base);
       HIPTRY(hipGetLastError());
     }
     P.order = (const uint32_t*)lpt_order.p;
@@ -595,21 +598,13 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
     wgt::TransportParams PS{}, PO{};
     uint32_t gs = 0, go = 0;
     bool os = false, oo = false;
-    // dynamic claims (WG_CLAIM): mixed lengths on the persistent 8-lane plan, with a grid that the
-    // sub-order count divides (claim_nc: the largest power of two <= 64 dividing it)
+    // dynamic claims (WG_CLAIM): mixed lengths on the persistent 8-lane plan with at least two packets
+    // per slot (the same test plan_transport makes for its longest-first pairs); up to 64 sub-orders,
+    // plan_transport picks how many divide its grid
     uint32_t claim_nc = 0;
-    if (c->claim && !(sb->flags & WG_F_UNIFORM) && sp.split == 0 && G == 8) {
-      const uint32_t spw = 8u;
-      const uint64_t cap_slots = spw * cap;
-      const uint64_t per_slot = 2ull * sb->n > cap_slots ? 2 * ((sb->n + cap_slots - 1) / cap_slots) : 1;
-      const uint32_t waves = (uint32_t)((sb->n + spw * per_slot - 1) / (spw * per_slot));
-      const uint32_t grid = (waves + wgt::TW - 1) / wgt::TW;
+    if (c->claim && !(sb->flags & WG_F_UNIFORM) && sp.split == 0 && G == 8 && 2ull * sb->n > 8ull * cap &&
+        c->lpt_claim.ensure(64u * 64u) == WG_OK && c->lpt_chain.ensure(sizeof(uint2) * (size_t)sb->n) == WG_OK)
       claim_nc = 64;
-      while (claim_nc > 1 && grid % claim_nc) claim_nc >>= 1;
-      if (per_slot < 2 || (rc = c->lpt_claim.ensure(64u * 64u)) != WG_OK ||
-          (rc = c->lpt_chain.ensure(sizeof(uint2) * (size_t)sb->n)) != WG_OK)
-        claim_nc = 0;
-    }
     rc = plan_transport<WG_MODE_SEAL>(c, sb->desc, sb->n, sb->in, sb->in_size, sb->out, sb->out_size, nullptr,
                                       sb->max_len, sb->flags, s, cap, G, c->lpt_hist, c->lpt_order, &PS, &gs, &os,
                                       nullptr, true, false, sp.split, claim_nc ? (uint32_t*)c->lpt_claim.p : nullptr,
@@ -622,7 +617,7 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
     if (PS.prio_step) PS.prio_step = PO.prio_step = 2u * PS.prio_step;
     if (claim_nc) {
       PS.chain_out = (uint2*)c->lpt_chain.p;
-      PO.claim_nc = claim_nc;  // the open half replays the seal's log from the same first positions
+      PO.claim_nc = PS.claim_nc;  // the open half replays the seal's log from the same first positions
       PO.chain_in = (const uint2*)c->lpt_chain.p;
     }
     if (rc == WG_OK && (gs != go || PS.slots != PO.slots || PS.order != PO.order))
