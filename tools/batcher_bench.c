@@ -40,6 +40,7 @@ static int g_gap_us;
 static double g_held_us = -1.0;
 static int g_held_rc = 0;
 static int g_stamps;
+static int g_pinned = -1; /* the NUMA node every thread runs on, -1: not pinned */
 typedef struct {
   double lat_us;
   uint64_t st[8];   /* wg_pp_last_call */
@@ -125,6 +126,30 @@ static void* held(void* arg) {
   return NULL;
 }
 
+/* the CPUs of NUMA node `node` from sysfs ("0-63,128-191"); 0 if unreadable */
+static int node_cpus(int node, cpu_set_t* set) {
+  char path[96], buf[4096];
+  if (node < 0) return 0;
+  snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+  FILE* f = fopen(path, "r");
+  if (!f) return 0;
+  const int ok = fgets(buf, sizeof buf, f) != NULL;
+  fclose(f);
+  if (!ok) return 0;
+  CPU_ZERO(set);
+  int n = 0;
+  for (char* p = buf; *p && *p != '\n';) {
+    char* e;
+    const long a = strtol(p, &e, 10);
+    if (e == p) break;
+    long b = a;
+    if (*e == '-') b = strtol(e + 1, &e, 10);
+    for (long c = a; c <= b && c < CPU_SETSIZE; ++c, ++n) CPU_SET((int)c, set);
+    p = *e == ',' ? e + 1 : e;
+  }
+  return n;
+}
+
 static int cmpd(const void* a, const void* b) {
   double x = *(const double*)a, y = *(const double*)b;
   return x < y ? -1 : x > y;
@@ -174,6 +199,15 @@ int main(int argc, char** argv) {
   if (fail_launches) {
     snprintf(buf, sizeof buf, "%d", fail_launches);
     setenv("WG_PP_TEST_FAIL_LAUNCHES", buf, 1);
+  }
+  /* every thread on the GPU's NUMA node (BB_PIN=0: wherever the scheduler puts them), before the
+   * context and its rings exist: a caller on the other socket adds a cross-socket snoop to every
+   * device read of the payload it just wrote (about 0.7 us) and to its own completion polls */
+  const char* pin = getenv("BB_PIN");
+  cpu_set_t set;
+  if ((!pin || atoi(pin) != 0) && node_cpus(wg_device_numa_node(0), &set)) {
+    pthread_setaffinity_np(pthread_self(), sizeof set, &set);  /* threads created later inherit it */
+    g_pinned = wg_device_numa_node(0);
   }
   if (wg_ctx_create(0, 64, &g_ctx) != WG_OK) {
     fprintf(stderr, "wg_ctx_create: %s\n", wg_last_error());
@@ -248,12 +282,13 @@ int main(int argc, char** argv) {
          "\"calls\": %zu, \"failures\": %d, \"wall_s\": %.4f, \"calls_per_s\": %.0f, "
          "\"payload_gib_s\": %.4f, \"lat_us\": {\"p50\": %.1f, \"p90\": %.1f, \"p99\": %.1f, \"p999\": %.1f, "
          "\"max\": %.1f}, \"launches\": %llu, \"mean_batch\": %.1f, \"gap_us\": %d, \"waves\": %d, "
-         "\"fail_launches\": %d, \"hold_us\": %d, \"held_us\": %.1f, \"held_rc\": %d, \"throttled_periods\": %llu%s}\n",
+         "\"fail_launches\": %d, \"hold_us\": %d, \"held_us\": %.1f, \"held_rc\": %d, \"throttled_periods\": %llu, "
+         "\"pinned_node\": %d%s}\n",
          T, g_calls, g_len ? argv[3] : "mixed 64..1500", n, fails, wall * 1e-6, n / (wall * 1e-6),
          bytes / (wall * 1e-6) / (double)(1u << 30), g_lat[n / 2], g_lat[n * 9 / 10], g_lat[n * 99 / 100],
          g_lat[n * 999 / 1000], g_lat[n - 1], (unsigned long long)(l1 - l0),
          (l1 > l0) ? (double)(p1 - p0) / (double)(l1 - l0) : 0.0, g_gap_us, waves, fail_launches, hold_us,
-         g_held_us, g_held_rc, thr1 - thr0, slow);
+         g_held_us, g_held_rc, thr1 - thr0, g_pinned, slow);
   wg_ctx_destroy(g_ctx);
   return (fails || g_held_rc) ? 1 : 0;
 }
