@@ -368,6 +368,11 @@ int wg_open_host(wg_ctx* ctx, const wg_pkt* desc_host, uint32_t n, const uint8_t
  *     use (until the consumer calls wg_reap_done), and then at most the queue's submit timeout:
  *     returns WG_EAGAIN after it. Thread-safe: any number of producers.
  *   wg_submit_open(q, key_slot, counter, ct_tag, len, user): the same for ct || tag (len + 16 B).
+ *   wg_submit_seal_n / wg_submit_open_n(q, p, n): n packets in one call, as n wg_submit_* calls in
+ *     order from one thread, but with one lane lock and one publication per run of free slots.
+ *     Returns how many were queued: n, or fewer (at least 1) when the submit timeout ran out
+ *     partway; WG_EAGAIN when it ran out before the first. Every entry is checked first: a bad one
+ *     fails the call (WG_EINVAL / WG_E2BIG / WG_ERANGE) with nothing queued.
  *   wg_reap(q, out, max, timeout_us): up to max completions (waits up to timeout_us for the
  *     first); returns how many, or a negative error. completion.data points into the queue's
  *     pinned ring: ct || tag (len + 16 B) for a seal, the plaintext (len B, valid when status is
@@ -399,6 +404,15 @@ int wg_queue_destroy(wg_queue* q);
 int wg_submit_seal(wg_queue* q, uint32_t key_slot, uint64_t counter, const uint8_t* pt, uint32_t len, uint64_t user);
 int wg_submit_open(wg_queue* q, uint32_t key_slot, uint64_t counter, const uint8_t* ct_tag, uint32_t len,
                    uint64_t user);
+typedef struct wg_submit {
+  uint64_t user;        /* the submitter's tag (echoed in the completion) */
+  uint64_t counter;     /* nonce = LE64(counter) || 0^4 */
+  const uint8_t* data;  /* seal: the plaintext (len B); open: ct || tag (len + 16 B) */
+  uint32_t len;         /* payload bytes */
+  uint32_t key_slot;
+} wg_submit;
+int wg_submit_seal_n(wg_queue* q, const wg_submit* p, uint32_t n);
+int wg_submit_open_n(wg_queue* q, const wg_submit* p, uint32_t n);
 int wg_reap(wg_queue* q, wg_completion* out, uint32_t max, uint32_t timeout_us);
 int wg_reap_done(wg_queue* q, const wg_completion* done, uint32_t n);
 int wg_queue_stats(wg_queue* q, uint64_t* batches, uint64_t* packets);

@@ -324,6 +324,117 @@ def test_queue_beside_batch_calls_with_timing_and_another_kernel():
         eng.close()
 
 
+@pytest.mark.gpu
+def test_batched_submits_bit_exact_beside_single_submits():
+    """wg_submit_seal_n / wg_submit_open_n: 3 producer threads submit 2,000 packets of 0..1500 B each in
+    runs of 1..300 (more than a lane's share of the 1,024-slot ring, so runs span several free-slot
+    runs and wait for the consumer), a fourth submits one at a time; every sealed packet matches the
+    oracle, then the forwarder shape: reaped completions submitted to an open queue in batches of
+    what one wg_reap returned, every plaintext equal to the input."""
+    W = wg()
+    eng = W.Engine(0, key_slots=8)
+    qs = qo = None
+    try:
+        keys = splitmix_np(2701, 32 * 8)
+        eng.set_keys(0, keys.tobytes())
+        qs, qo = eng.queue("seal", capacity=1024), eng.queue("open", capacity=1024)
+        T, N = 4, 2000
+        sent, errors, lock = {}, [], threading.Lock()
+
+        def producer(t):
+            try:
+                rng = np.random.default_rng(40 + t)
+                i = 0
+                while i < N:
+                    run = 1 if t == 3 else int(rng.integers(1, 301))
+                    batch = []
+                    for _ in range(min(run, N - i)):
+                        L = int(rng.integers(0, 1501))
+                        user = (t << 32) | i
+                        pt = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+                        with lock:
+                            sent[user] = (i % 8, (t << 40) | i, pt)
+                        batch.append((i % 8, (t << 40) | i, pt, user))
+                        i += 1
+                    if t == 3:
+                        qs.submit(*batch[0])
+                    else:
+                        assert qs.submit_n(batch) == len(batch)
+            except Exception as e:  # pragma: no cover - reported by the reaping loop
+                errors.append(repr(e))
+
+        got, stop = {}, threading.Event()
+
+        def consumer():  # the open queue's reaper (the forwarder below outruns its 1,024 slots)
+            try:
+                while not stop.is_set() and len(got) < T * N:
+                    for user, ctr, st, data in qo.reap(4096, 20000):
+                        got[user] = (ctr, st, data)
+            except Exception as e:  # pragma: no cover - reported below
+                errors.append(repr(e))
+
+        th = [threading.Thread(target=producer, args=(t,), daemon=True) for t in range(T)]
+        rc = threading.Thread(target=consumer, daemon=True)
+        for x in th + [rc]:
+            x.start()
+        sealed = {}
+        deadline = time.monotonic() + 60
+        while len(sealed) < T * N:
+            assert not errors, errors[:3]
+            assert time.monotonic() < deadline, (len(sealed), qs.stats())
+            done = qs.reap(4096, 200000)
+            for user, ctr, st, data in done:
+                assert st == 0, st
+                sealed[user] = (ctr, data)
+            # forward what this reap returned to the open queue in one call
+            if done:
+                assert qo.submit_n([(sent[u][0], c, d, u) for u, c, _, d in done]) == len(done)
+        for x in th:
+            x.join()
+        for user, (slot, ctr, pt) in sent.items():
+            key = keys[32 * slot:32 * slot + 32].tobytes()
+            assert sealed[user] == (ctr, O.c_aead_seal(key, O.transport_nonce(ctr), pt)), user
+        rc.join(timeout=60)
+        stop.set()
+        assert not errors, errors[:3]
+        assert len(got) == T * N, (len(got), qo.stats())
+        for user, (slot, ctr, pt) in sent.items():
+            assert got[user] == (ctr, 0, pt), user
+    finally:
+        for q in (qs, qo):
+            if q is not None:
+                q.close()
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_batched_submit_stops_at_the_timeout_and_checks_every_entry_first():
+    """A 64-slot queue nobody reaps: a batch of 100 queues 64 and returns 64 once the 5-ms submit timeout
+    runs out; the next batch gets WG_EAGAIN; a batch with one oversized entry queues nothing."""
+    W = wg()
+    eng = W.Engine(0, key_slots=1)
+    q = None
+    try:
+        eng.set_keys(0, splitmix_bytes(2801, 32))
+        q = eng.queue("seal", capacity=64, max_len=256)
+        q.set_submit_timeout(5000)
+        with pytest.raises(W.WgError) as ei:
+            q.submit_n([(0, 0, b"a" * 16, 0), (0, 1, b"b" * 300, 1)])
+        assert ei.value.code == W._lib.WG_E2BIG
+        t0 = time.monotonic()
+        assert q.submit_n([(0, i, bytes([i]) * 32, i) for i in range(100)]) == 64
+        assert time.monotonic() - t0 < 2.0
+        with pytest.raises(W.WgError) as ei:
+            q.submit_n([(0, 100, b"z", 100)])
+        assert ei.value.code == W._lib.WG_EAGAIN
+        got = _reap_all(q, 64)
+        assert sorted(got) == list(range(64)) and all(st == 0 for _, st, _ in got.values())
+    finally:
+        if q is not None:
+            q.close()
+        eng.close()
+
+
 def test_queue_argument_contract():
     W = wg()
     lib = W.lib()
@@ -333,6 +444,8 @@ def test_queue_argument_contract():
     assert lib.wg_queue_create(None, 0, 0, 0, 0, ctypes.byref(q)) == E
     assert lib.wg_submit_seal(None, 0, 0, None, 0, 0) == E
     assert lib.wg_submit_open(None, 0, 0, None, 0, 0) == E
+    assert lib.wg_submit_seal_n(None, None, 0) == E
+    assert lib.wg_submit_open_n(None, None, 0) == E
     assert lib.wg_reap(None, None, 0, 0) == E
     assert lib.wg_reap_done(None, None, 0) == E
     assert lib.wg_queue_stats(None, None, None) == E

@@ -7,7 +7,7 @@
  *
  * Build: make -C tools queue_bench
  * Run:   tools/queue_bench [producers=16] [packets_per_producer=200000] [len=1420|0 mixed 64..1500]
- *                          [max_batch=8192] [forwarders=1] [verifiers=1] [cpu_port=PATH]
+ *                          [max_batch=8192] [forwarders=1] [verifiers=1] [cpu_port=PATH] [fwd_batch=1]
  * cpu_port=oracle/liboracle.so: after the queue run, the CPU restatement of the reference's AEAD seals
  * and opens the SAME packets (lengths, keys, counters) on `producers` threads, in the same process and
  * run, so the line compares the queue with the CPU port on exactly this packet mix ("cpu_port_gib_s").
@@ -84,9 +84,12 @@ static void* producer(void* arg) {
   return NULL;
 }
 
+static int g_fwd_batch; /* fwd_batch=1: the forwarder hands each reap's completions over in one wg_submit_open_n */
+
 static void* forwarder(void* arg) {
   (void)arg;
   wg_completion c[1024];
+  wg_submit sub[1024];
   while (atomic_load(&g_fwd) < g_total) {
     const int n = wg_reap(g_qs, c, 1024, 1000);
     if (n < 0) {
@@ -94,15 +97,21 @@ static void* forwarder(void* arg) {
       exit(1);
     }
     const uint64_t now = now_ns();
+    const uint64_t j0 = atomic_fetch_add(&g_ns, (uint64_t)(n > 0 ? n : 0));
     for (int k = 0; k < n; ++k) {
       if (c[k].status != WG_PKT_OK) atomic_fetch_add(&g_bad, 1);
-      const uint64_t j = atomic_fetch_add(&g_ns, 1);
-      if (j < LAT_SAMPLES) g_lat_s[j] = (now - c[k].submit_ns) * 1e-3;
+      if (j0 + k < LAT_SAMPLES) g_lat_s[j0 + k] = (now - c[k].submit_ns) * 1e-3;
       /* ct || tag as it would arrive at the peer */
-      if (wg_submit_open(g_qo, c[k].key_slot, c[k].counter, c[k].data, c[k].len, c[k].user) != WG_OK) {
+      if (g_fwd_batch) {
+        sub[k] = (wg_submit){c[k].user, c[k].counter, c[k].data, c[k].len, c[k].key_slot};
+      } else if (wg_submit_open(g_qo, c[k].key_slot, c[k].counter, c[k].data, c[k].len, c[k].user) != WG_OK) {
         fprintf(stderr, "submit_open: %s\n", wg_last_error());
         exit(1);
       }
+    }
+    if (g_fwd_batch && n > 0 && wg_submit_open_n(g_qo, sub, (uint32_t)n) != n) {  /* one call per reap */
+      fprintf(stderr, "submit_open_n: %s\n", wg_last_error());
+      exit(1);
     }
     wg_reap_done(g_qs, c, (uint32_t)n);
     atomic_fetch_add(&g_fwd, (uint64_t)n);
@@ -121,9 +130,9 @@ static void* verifier(void* arg) {
       exit(1);
     }
     const uint64_t now = now_ns();
+    const uint64_t j0 = atomic_fetch_add(&g_no, (uint64_t)(n > 0 ? n : 0));
     for (int k = 0; k < n; ++k) {
-      const uint64_t j = atomic_fetch_add(&g_no, 1);
-      if (j < LAT_SAMPLES) g_lat_o[j] = (now - c[k].submit_ns) * 1e-3;
+      if (j0 + k < LAT_SAMPLES) g_lat_o[j0 + k] = (now - c[k].submit_ns) * 1e-3;
       fill(want, c[k].user, c[k].len);
       if (c[k].status != WG_PKT_OK || c[k].len != pkt_len(c[k].user) || memcmp(c[k].data, want, c[k].len) != 0)
         atomic_fetch_add(&g_bad, 1);
@@ -203,8 +212,10 @@ int main(int argc, char** argv) {
   const int max_batch = argc > 4 ? atoi(argv[4]) : 8192;
   const int nf = argc > 5 ? atoi(argv[5]) : 1, nv = argc > 6 ? atoi(argv[6]) : 1;
   const char* cpu_port = NULL;
-  for (int a = 1; a < argc; ++a)
+  for (int a = 1; a < argc; ++a) {
     if (!strncmp(argv[a], "cpu_port=", 9)) cpu_port = argv[a] + 9;
+    if (!strncmp(argv[a], "fwd_batch=", 10)) g_fwd_batch = atoi(argv[a] + 10);
+  }
   if (g_P < 1 || g_P > 256 || g_N < 1 || g_len < 0 || g_len > 1500) {
     fprintf(stderr, "usage: queue_bench [producers] [packets_per_producer] [len 0..1500] [max_batch]\n");
     return 2;
@@ -324,12 +335,12 @@ int main(int argc, char** argv) {
          "\"seal_lat_us\": {\"p50\": %.1f, \"p99\": %.1f, \"p999\": %.1f, \"max\": %.1f}, "
          "\"open_lat_us\": {\"p50\": %.1f, \"p99\": %.1f, \"p999\": %.1f, \"max\": %.1f}, "
          "\"seal_batches\": %llu, \"seal_mean_batch\": %.1f, \"open_batches\": %llu, \"open_mean_batch\": %.1f, "
-         "\"cpu_s\": %.3f, \"cpus_busy\": %.2f, \"throttled_periods\": %llu, \"throttled_ms\": %.1f, \"pinned_node\": %d%s}\n",
+         "\"cpu_s\": %.3f, \"cpus_busy\": %.2f, \"throttled_periods\": %llu, \"throttled_ms\": %.1f, \"pinned_node\": %d, \"fwd_batch\": %d%s}\n",
          g_P, nf, nv, (unsigned long long)g_total, g_len ? argv[3] : "mixed 64..1500", max_batch,
          (unsigned long long)g_bad, wall, 2.0 * bytes / wall / gib, bytes / t_sealed / gib, bytes / t_submit / gib,
          g_total / wall, ls[0], ls[1], ls[2], ls[3], lo[0], lo[1], lo[2], lo[3], (unsigned long long)bs,
          bs ? (double)ps / bs : 0.0, (unsigned long long)bo, bo ? (double)po / bo : 0.0, cpu, cpu / wall,
-         thp1 - thp0, (thu1 - thu0) * 1e-3, pinned, cpu_json);
+         thp1 - thp0, (thu1 - thu0) * 1e-3, pinned, g_fwd_batch, cpu_json);
   wg_queue_destroy(g_qs);
   wg_queue_destroy(g_qo);
   wg_ctx_destroy(g_ctx);

@@ -88,7 +88,13 @@ class WgCompletion(ctypes.Structure):
                 ("slot", ctypes.c_uint32), ("submit_ns", ctypes.c_uint64)]
 
 
-assert ctypes.sizeof(WgBatch) == 64 and ctypes.sizeof(WgCompletion) == 48
+class WgSubmit(ctypes.Structure):
+    """wg_submit: one packet of wg_submit_seal_n / wg_submit_open_n."""
+    _fields_ = [("user", ctypes.c_uint64), ("counter", ctypes.c_uint64), ("data", ctypes.c_void_p),
+                ("len", ctypes.c_uint32), ("key_slot", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(WgBatch) == 64 and ctypes.sizeof(WgCompletion) == 48 and ctypes.sizeof(WgSubmit) == 32
 assert ctypes.sizeof(WgPkt) == 32 and ctypes.sizeof(WgAeadDesc) == 64 and ctypes.sizeof(WgPrefix) == 18
 
 # (name, restype, argtypes) for every symbol include/wgaead.h declares
@@ -130,6 +136,8 @@ SIGNATURES = [
     ("wg_queue_destroy", _I, [_VP]),
     ("wg_submit_seal", _I, [_VP, _U32, _U64, _VP, _U32, _U64]),
     ("wg_submit_open", _I, [_VP, _U32, _U64, _VP, _U32, _U64]),
+    ("wg_submit_seal_n", _I, [_VP, ctypes.POINTER(WgSubmit), _U32]),
+    ("wg_submit_open_n", _I, [_VP, ctypes.POINTER(WgSubmit), _U32]),
     ("wg_reap", _I, [_VP, ctypes.POINTER(WgCompletion), _U32, _U32]),
     ("wg_reap_done", _I, [_VP, ctypes.POINTER(WgCompletion), _U32]),
     ("wg_queue_stats", _I, [_VP, ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),

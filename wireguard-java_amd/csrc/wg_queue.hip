@@ -444,24 +444,17 @@ int queue_try_slot(wg_queue* q, wgq::Lane& ln, uint32_t* s) {
   return r;
 }
 
-int queue_submit(wg_queue* q, int mode, uint32_t key_slot, uint64_t counter, const uint8_t* src, uint32_t len,
-                 uint64_t user) {
-  if (!q || (!src && (len || mode == WG_MODE_OPEN))) return fail(WG_EINVAL, "NULL argument");
-  if (q->mode != mode) return fail(WG_EINVAL, "a %s queue", q->mode == WG_MODE_SEAL ? "seal" : "open");
-  if (len > q->max_len) return fail(WG_E2BIG, "packet of %u bytes > the queue's max_len %u", len, q->max_len);
-  if (key_slot >= q->c->key_slots) return fail(WG_ERANGE, "key slot %u", key_slot);
-  if (const int e = q->err.load(std::memory_order_relaxed)) return fail(e, "queue failed earlier");
-  wgq::Lane& ln = q->lane[wgq::thread_number() % q->lanes];
-  uint32_t s = 0;
-  uint64_t deadline = 0;  // wg_queue_set_submit_timeout: WG_EAGAIN once no slot was free for that long
+// A free slot for lane `ln`, its lock held on return (WG_OK), waiting as the queue's submit policy says:
+// WG_EAGAIN once none was free for the submit timeout (*deadline: 0 before the first wait).
+int queue_acquire(wg_queue* q, wgq::Lane& ln, uint32_t* s, uint64_t* deadline) {
   for (uint32_t round = 0;; ++round) {
     const uint32_t w = q->wake_word.load(std::memory_order_acquire);
-    const int r = queue_try_slot(q, ln, &s);
-    if (r == 1) break;
+    const int r = queue_try_slot(q, ln, s);
+    if (r == 1) return WG_OK;
     if (q->submit_timeout_ns) {
       const uint64_t now = wgq::now_ns();
-      if (!deadline) deadline = now + q->submit_timeout_ns;
-      else if (now >= deadline)
+      if (!*deadline) *deadline = now + q->submit_timeout_ns;
+      else if (now >= *deadline)
         return fail(WG_EAGAIN, "no free queue slot for %llu us (is the consumer calling wg_reap_done?)",
                     (unsigned long long)(q->submit_timeout_ns / 1000u));
     }
@@ -473,14 +466,19 @@ int queue_submit(wg_queue* q, int mode, uint32_t key_slot, uint64_t counter, con
       continue;
     }
     q->free_waiters.fetch_add(1, std::memory_order_seq_cst);
-    if (queue_try_slot(q, ln, &s) == 1) {  // freed before this thread counted as a waiter
+    if (queue_try_slot(q, ln, s) == 1) {  // freed before this thread counted as a waiter
       q->free_waiters.fetch_sub(1, std::memory_order_relaxed);
-      break;
+      return WG_OK;
     }
     const struct timespec ts = {0, 1000000};  // 1 ms: the last slots of a burst wake nobody
     futex(&q->wake_word, FUTEX_WAIT_PRIVATE, w, &ts);
     q->free_waiters.fetch_sub(1, std::memory_order_relaxed);
   }
+}
+
+// Fill slot s with one packet: its key as the key slot holds it now, its meta, its bytes.
+void queue_fill(wg_queue* q, uint32_t s, uint32_t key_slot, uint64_t counter, const uint8_t* src, uint32_t len,
+                uint64_t user) {
   key_snapshot(q->c, key_slot, q->h_key + 8ull * s);
   wgq::SlotMeta& m = q->meta[s];
   m.user = user;
@@ -488,11 +486,14 @@ int queue_submit(wg_queue* q, int mode, uint32_t key_slot, uint64_t counter, con
   m.len = len;
   m.key_slot = key_slot;
   m.t_submit_ns = wgq::now_ns();
-  const size_t n = (size_t)len + (mode == WG_MODE_OPEN ? 16u : 0u);
+  const size_t n = (size_t)len + (q->mode == WG_MODE_OPEN ? 16u : 0u);
   if (n) memcpy(q->h_in + (size_t)s * q->stride, src, n);
-  const uint64_t rt = ln.r_tail.load(std::memory_order_relaxed);
-  ln.ready[rt % q->per_lane] = s;
-  ln.r_tail.store(rt + 1, std::memory_order_release);  // publish: after the slot's bytes and meta
+}
+
+// Publish the lane's ready entries up to rt (its lock held; released here) and wake the dispatcher
+// if it sleeps.
+void queue_publish(wg_queue* q, wgq::Lane& ln, uint64_t rt) {
+  ln.r_tail.store(rt, std::memory_order_release);  // after the slots' bytes and meta
   wgq::spin_unlock(ln.lock);
   // (no shared per-packet counter: 16 producers incrementing one cache line per packet serialised on it)
   std::atomic_thread_fence(std::memory_order_seq_cst);
@@ -500,7 +501,69 @@ int queue_submit(wg_queue* q, int mode, uint32_t key_slot, uint64_t counter, con
     std::lock_guard<std::mutex> lk(q->mu);
     q->cv_disp.notify_one();
   }
+}
+
+int queue_check(wg_queue* q, int mode) {
+  if (!q) return fail(WG_EINVAL, "NULL queue");
+  if (q->mode != mode) return fail(WG_EINVAL, "a %s queue", q->mode == WG_MODE_SEAL ? "seal" : "open");
+  if (const int e = q->err.load(std::memory_order_relaxed)) return fail(e, "queue failed earlier");
   return WG_OK;
+}
+
+int queue_check_packet(wg_queue* q, int mode, uint32_t key_slot, const uint8_t* src, uint32_t len) {
+  if (!src && (len || mode == WG_MODE_OPEN)) return fail(WG_EINVAL, "NULL argument");
+  if (len > q->max_len) return fail(WG_E2BIG, "packet of %u bytes > the queue's max_len %u", len, q->max_len);
+  if (key_slot >= q->c->key_slots) return fail(WG_ERANGE, "key slot %u", key_slot);
+  return WG_OK;
+}
+
+int queue_submit(wg_queue* q, int mode, uint32_t key_slot, uint64_t counter, const uint8_t* src, uint32_t len,
+                 uint64_t user) {
+  int rc;
+  if ((rc = queue_check(q, mode)) != WG_OK || (rc = queue_check_packet(q, mode, key_slot, src, len)) != WG_OK)
+    return rc;
+  wgq::Lane& ln = q->lane[wgq::thread_number() % q->lanes];
+  uint32_t s = 0;
+  uint64_t deadline = 0;  // wg_queue_set_submit_timeout: WG_EAGAIN once no slot was free for that long
+  if ((rc = queue_acquire(q, ln, &s, &deadline)) != WG_OK) return rc;
+  queue_fill(q, s, key_slot, counter, src, len, user);
+  const uint64_t rt = ln.r_tail.load(std::memory_order_relaxed);
+  ln.ready[rt % q->per_lane] = s;
+  queue_publish(q, ln, rt + 1);
+  return WG_OK;
+}
+
+// n packets in one call: one lane lock, one publication and one dispatcher check per run of free
+// slots instead of per packet (the forwarder of tools/queue_bench spends its time in exactly that
+// per-packet overhead on small packets). Returns how many were queued, in order: n, or fewer when
+// the submit timeout ran out (none: WG_EAGAIN). A bad entry fails the call before anything is queued.
+int queue_submit_n(wg_queue* q, int mode, const wg_submit* p, uint32_t n) {
+  int rc;
+  if ((rc = queue_check(q, mode)) != WG_OK) return rc;
+  if (!p && n) return fail(WG_EINVAL, "NULL argument");
+  if (n > (uint32_t)INT32_MAX) return fail(WG_EINVAL, "%u packets", n);
+  for (uint32_t k = 0; k < n; ++k)
+    if ((rc = queue_check_packet(q, mode, p[k].key_slot, p[k].data, p[k].len)) != WG_OK) return rc;
+  wgq::Lane& ln = q->lane[wgq::thread_number() % q->lanes];
+  uint64_t deadline = 0;
+  uint32_t k = 0;
+  while (k < n) {
+    uint32_t s = 0;
+    if ((rc = queue_acquire(q, ln, &s, &deadline)) != WG_OK) return k ? (int)k : rc;
+    uint64_t rt = ln.r_tail.load(std::memory_order_relaxed);
+    const uint64_t rh = ln.r_head.load(std::memory_order_acquire);
+    for (;;) {
+      queue_fill(q, s, p[k].key_slot, p[k].counter, p[k].data, p[k].len, p[k].user);
+      ln.ready[rt % q->per_lane] = s;
+      ++rt;
+      ++k;
+      // the lane's ready ring holds at most per_lane entries (queue_try_slot's bound)
+      if (k == n || rt - rh >= q->per_lane || !queue_take_slot(q, ln, &s)) break;
+    }
+    queue_publish(q, ln, rt);
+    deadline = 0;  // the timeout bounds each wait for a free slot, as for single submits
+  }
+  return (int)n;
 }
 
 uint32_t pow2_at_least(uint32_t v) {
@@ -632,6 +695,10 @@ int wg_submit_open(wg_queue* q, uint32_t key_slot, uint64_t counter, const uint8
                    uint64_t user) {
   return queue_submit(q, WG_MODE_OPEN, key_slot, counter, ct_tag, len, user);
 }
+
+int wg_submit_seal_n(wg_queue* q, const wg_submit* p, uint32_t n) { return queue_submit_n(q, WG_MODE_SEAL, p, n); }
+
+int wg_submit_open_n(wg_queue* q, const wg_submit* p, uint32_t n) { return queue_submit_n(q, WG_MODE_OPEN, p, n); }
 
 int wg_reap(wg_queue* q, wg_completion* out, uint32_t max, uint32_t timeout_us) {
   if (!q || (!out && max)) return fail(WG_EINVAL, "NULL argument");

@@ -381,6 +381,23 @@ class Queue:
         fn = self._lib.wg_submit_seal if self.mode == L.WG_MODE_SEAL else self._lib.wg_submit_open
         L.check(fn(self.q, key_slot, counter, src.ctypes.data, n, user))
 
+    def submit_n(self, packets) -> int:
+        """wg_submit_seal_n / wg_submit_open_n: packets = [(key_slot, counter, data, user)] queued in
+        one call (data as for submit()); returns how many were queued (fewer than len(packets) only
+        when the submit timeout ran out partway)."""
+        arr = (L.WgSubmit * max(1, len(packets)))()
+        keep = []
+        for k, (key_slot, counter, data, user) in enumerate(packets):
+            n = len(data) - (16 if self.mode == L.WG_MODE_OPEN else 0)
+            if n < 0:
+                raise ValueError("open needs ct || tag (at least 16 bytes)")
+            src = np.frombuffer(bytes(data), np.uint8) if data else np.zeros(1, np.uint8)
+            keep.append(src)
+            arr[k].user, arr[k].counter, arr[k].data = user, counter, src.ctypes.data
+            arr[k].len, arr[k].key_slot = n, key_slot
+        fn = self._lib.wg_submit_seal_n if self.mode == L.WG_MODE_SEAL else self._lib.wg_submit_open_n
+        return L.check(fn(self.q, arr, len(packets)))
+
     def reap(self, max_n: int = 4096, timeout_us: int = 100000):
         """[(user, counter, status, result bytes)], the slots handed back at once; the result is
         ct || tag for a seal, the plaintext for an open (None unless status is WG_PKT_OK)."""

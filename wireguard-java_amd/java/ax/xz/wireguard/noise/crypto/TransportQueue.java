@@ -29,6 +29,8 @@ import static java.lang.foreign.ValueLayout.*;
 public final class TransportQueue implements AutoCloseable {
 	/** wg_completion: {user u64, counter u64, data ptr, len u32, status u32, key_slot u32, slot u32, submit_ns u64}. */
 	static final long COMPLETION_SIZE = 48;
+	/** wg_submit: {user u64, counter u64, data ptr, len u32, key_slot u32}. */
+	static final long SUBMIT_SIZE = 32;
 
 	private final MemorySegment q;
 	private final boolean open;
@@ -64,6 +66,31 @@ public final class TransportQueue implements AutoCloseable {
 		try {
 			WgAead.check(open ? (int) WgAead.SUBMIT_OPEN.invokeExact(q, keySlot, counter, src, len, user)
 			                  : (int) WgAead.SUBMIT_SEAL.invokeExact(q, keySlot, counter, src, len, user));
+		} catch (RuntimeException e) {
+			throw e;
+		} catch (Throwable e) {
+			throw new RuntimeException(e);
+		}
+	}
+
+	/**
+	 * Queue n packets in one call (wg_submit_seal_n / wg_submit_open_n: one lane lock and one publication
+	 * per run of free slots instead of per packet), e.g. everything one receive burst or one reap() of the
+	 * peer's queue returned. Returns how many were queued: n, or fewer when the submit timeout ran out.
+	 */
+	public int submitAll(int[] keySlots, long[] counters, MemorySegment[] srcs, long[] users, int n) {
+		try (var a = Arena.ofConfined()) {
+			var sub = a.allocate(SUBMIT_SIZE * Math.max(n, 1), 16);
+			for (int i = 0; i < n; i++) {
+				final long o = i * SUBMIT_SIZE;
+				sub.set(JAVA_LONG, o, users[i]);
+				sub.set(JAVA_LONG, o + 8, counters[i]);
+				sub.set(ADDRESS, o + 16, srcs[i]);
+				sub.set(JAVA_INT, o + 24, (int) srcs[i].byteSize() - (open ? 16 : 0));
+				sub.set(JAVA_INT, o + 28, keySlots[i]);
+			}
+			return WgAead.check(open ? (int) WgAead.SUBMIT_OPEN_N.invokeExact(q, sub, n)
+			                         : (int) WgAead.SUBMIT_SEAL_N.invokeExact(q, sub, n));
 		} catch (RuntimeException e) {
 			throw e;
 		} catch (Throwable e) {

@@ -38,7 +38,8 @@ public final class WgAead {
 	static final MethodHandle SELFTEST, CTX_CREATE, LAST_ERROR, KEYS_SET, KEYS_ZERO, SEAL1, OPEN1, AEAD_HOST,
 		SEAL_BATCH, OPEN_BATCH, SYNC, SEAL_HOST, OPEN_HOST, HOST_ALLOC, HOST_FREE, FRAME_SEAL, PARSE_OPEN,
 		FILTER_SET, SLOT_FILTERS_SET, REPLAY_ENABLE, REPLAY_RESET, RX_CHECK, DUPLEX_BATCH, QUEUE_CREATE,
-		QUEUE_DESTROY, SUBMIT_SEAL, SUBMIT_OPEN, REAP, REAP_DONE, QUEUE_SUBMIT_TIMEOUT, NUMA_NODE;
+		QUEUE_DESTROY, SUBMIT_SEAL, SUBMIT_OPEN, SUBMIT_SEAL_N, SUBMIT_OPEN_N, REAP, REAP_DONE, QUEUE_SUBMIT_TIMEOUT,
+		NUMA_NODE;
 
 	/** The process-wide context (one HIP device, its stream and its device key table). */
 	static final MemorySegment CTX;
@@ -98,6 +99,10 @@ public final class WgAead {
 			JAVA_LONG, ADDRESS, JAVA_INT, JAVA_LONG));
 		SUBMIT_OPEN = down(linker, symbols, "wg_submit_open", FunctionDescriptor.of(JAVA_INT, ADDRESS, JAVA_INT,
 			JAVA_LONG, ADDRESS, JAVA_INT, JAVA_LONG));
+		SUBMIT_SEAL_N = down(linker, symbols, "wg_submit_seal_n", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS,
+			JAVA_INT));
+		SUBMIT_OPEN_N = down(linker, symbols, "wg_submit_open_n", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS,
+			JAVA_INT));
 		REAP = down(linker, symbols, "wg_reap", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT, JAVA_INT));
 		REAP_DONE = down(linker, symbols, "wg_reap_done", FunctionDescriptor.of(JAVA_INT, ADDRESS, ADDRESS, JAVA_INT));
 		QUEUE_SUBMIT_TIMEOUT = down(linker, symbols, "wg_queue_set_submit_timeout", FunctionDescriptor.of(JAVA_INT,
