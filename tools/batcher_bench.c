@@ -48,6 +48,7 @@ typedef struct {
   int op, thread;
 } slow_t;
 static slow_t* g_slowest;        /* per thread */
+static double (*g_stage_sum)[5]; /* per thread: sums of claim, publish, wait, device service, copy-out (ns) */
 static int* g_over1ms, *g_over1ms_preempted;
 
 static double now_us(void) {
@@ -95,6 +96,7 @@ static void* worker(void* arg) {
         ++g_over1ms[t];
         if (niv > 0) ++g_over1ms_preempted[t];
       }
+      for (int k = 0; k < 5; ++k) g_stage_sum[t][k] += (double)st[k + 1];
       if (lat > g_slowest[t].lat_us) {
         g_slowest[t].lat_us = lat;
         memcpy(g_slowest[t].st, st, sizeof st);
@@ -225,6 +227,7 @@ int main(int argc, char** argv) {
   g_bytes = calloc(T, sizeof(uint64_t));
   g_fail = calloc(T, sizeof(int));
   g_slowest = calloc(T, sizeof(slow_t));
+  g_stage_sum = calloc(T, sizeof *g_stage_sum);
   g_over1ms = calloc(T, sizeof(int));
   g_over1ms_preempted = calloc(T, sizeof(int));
   pthread_t th[1024];
@@ -260,7 +263,7 @@ int main(int argc, char** argv) {
     bytes += g_bytes[t];
     fails += g_fail[t];
   }
-  char slow[768] = "";
+  char slow[1024] = "";
   if (g_stamps) {
     int w = 0, o1 = 0, o1p = 0;
     for (int t = 0; t < T; ++t) {
@@ -277,6 +280,13 @@ int main(int argc, char** argv) {
              x->lat_us, x->op ? "open" : "seal", x->thread, x->st[1] * 1e-3, x->st[2] * 1e-3, x->st[3] * 1e-3,
              x->st[4] * 1e-3, x->st[5] * 1e-3, (unsigned long long)x->st[6], (unsigned long long)x->st[7],
              x->nivcsw, x->nvcsw, o1, o1p);
+    double m[5] = {0, 0, 0, 0, 0};
+    for (int t = 0; t < T; ++t)
+      for (int k = 0; k < 5; ++k) m[k] += g_stage_sum[t][k] / ((double)T * g_calls) * 1e-3;
+    const size_t used = strlen(slow);
+    snprintf(slow + used, sizeof slow - used,
+             ", \"stage_mean_us\": {\"claim\": %.2f, \"publish\": %.2f, \"wait\": %.2f, \"device_service\": %.2f, "
+             "\"copy_out\": %.2f}", m[0], m[1], m[2], m[3], m[4]);
   }
   printf("{\"tool\": \"batcher_bench\", \"threads\": %d, \"calls_per_thread\": %d, \"len\": \"%s\", "
          "\"calls\": %zu, \"failures\": %d, \"wall_s\": %.4f, \"calls_per_s\": %.0f, "
