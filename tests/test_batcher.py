@@ -141,6 +141,56 @@ def test_per_packet_edges_bit_exact():
 
 
 @pytest.mark.gpu
+def test_per_packet_random_lengths_bit_exact():
+    """400 calls of random length 0..4080 in random order from two threads (a unit reads the whole slot
+    at once after a packet past 1,984 B, and its first 2 KB otherwise: every switch between the two,
+    both ways, and the second round trip), seal against the oracle and open back, every 7th open
+    with a forged tag that must leave the buffer untouched. Reference: ChaCha20Poly1305.java:31-60."""
+    import ctypes
+    W = wg()
+    eng = W.Engine(0, key_slots=2)
+    errors = []
+    try:
+        keys = splitmix_np(1901, 64)
+        eng.set_keys(0, keys.tobytes())
+        lib = W.lib()
+
+        def caller(t):
+            try:
+                rng = np.random.default_rng(190 + t)
+                for i in range(200):
+                    L = int(rng.choice([int(rng.integers(0, 4081)), int(rng.integers(1900, 2100)),
+                                        int(rng.integers(0, 64))]))
+                    slot = i % 2
+                    key = keys[32 * slot:32 * slot + 32].tobytes()
+                    ctr = (t << 40) | i
+                    pt = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+                    want = O.c_aead_seal(key, O.transport_nonce(ctr), pt)
+                    got = eng.seal1(slot, ctr, pt)
+                    assert got == want, (t, i, L)
+                    if i % 7 == 3:
+                        bad = bytearray(want)
+                        bad[L + (i % 16)] ^= 0x10
+                        src = (ctypes.c_uint8 * len(bad)).from_buffer_copy(bytes(bad))
+                        dst = (ctypes.c_uint8 * max(L, 1))(*([0x5C] * max(L, 1)))
+                        assert lib.wg_open1(eng.ctx, slot, ctr, src, L, dst) == 1, (t, i, L)
+                        assert bytes(dst) == b"\x5c" * max(L, 1), (t, i, L)
+                    else:
+                        assert eng.open1(slot, ctr, want) == pt, (t, i, L)
+            except Exception as e:  # pragma: no cover - reported below
+                errors.append(repr(e))
+
+        th = [threading.Thread(target=caller, args=(t,)) for t in range(2)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(timeout=120)
+        assert not errors, errors[:3]
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
 def test_new_context_while_another_server_runs():
     """A context created while another context's per-packet server is resident: its key table
     is zeroed on its own stream, so the first wg_keys_set is not overwritten by a late
