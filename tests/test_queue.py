@@ -147,11 +147,15 @@ def test_one_producer_uses_the_whole_ring():
 @pytest.mark.gpu
 def test_queue_c_harness_transport_manager_shape():
     """tools/queue_bench: 16 producer threads submit 1420-B packets to a seal queue, a forwarder
-    reaps them and submits each ct || tag to an open queue, a verifier checks every status and byte
-    of the plaintexts (the reference's FJP workers -> UDP worker -> peer -> tun writer)."""
+    reaps them and submits each ct || tag to an open queue (one by one, or per reap with
+    wg_submit_open_n), a verifier checks every status and byte of the plaintexts (the reference's FJP
+    workers -> UDP worker -> peer -> tun writer)."""
     exe = os.path.join(ROOT, "tools", "queue_bench")
     assert os.path.exists(exe), "tools/queue_bench is built by __graft_entry__.build()"
-    for args in (["16", "20000", "1420"], ["4", "20000", "0"]):
+    # the last two: two forwarders and two verifiers, each forwarder handing a whole reap to the open
+    # queue in one wg_submit_open_n (fwd_batch=1)
+    for args in (["16", "20000", "1420"], ["4", "20000", "0"], ["16", "20000", "0", "8192", "2", "2", "fwd_batch=1"],
+                 ["8", "20000", "1420", "8192", "1", "1", "fwd_batch=1"]):
         r = subprocess.run([exe] + args, capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-2000:])
         j = json.loads(r.stdout.strip().splitlines()[-1])
