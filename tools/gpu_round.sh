@@ -48,6 +48,9 @@ for k in 1 8; do
   timeout -k 10 200 ./tools/host_pipeline --backend gpu --packets 65536 --reps 5 --udp-streams $k --tun >> $O/host_pipeline_gpu.jsonl || die pipeline $?
 done
 timeout -k 10 300 ./tools/host_pipeline --backend cpu --oracle oracle/liboracle.so --threads 16 --packets 65536 --reps 3 --udp-streams 8 --tun >> $O/host_pipeline_cpu.jsonl || die pipeline_cpu $?
+# pipelined: seal, UDP and open overlap in 16 chunks
+timeout -k 10 200 ./tools/host_pipeline --backend gpu --packets 65536 --reps 5 --udp-streams 8 --chunks 16 >> $O/host_pipeline_gpu.jsonl || die pipeline_pipelined $?
+timeout -k 10 300 ./tools/host_pipeline --backend cpu --oracle oracle/liboracle.so --threads 16 --packets 65536 --reps 3 --udp-streams 8 --chunks 16 >> $O/host_pipeline_cpu.jsonl || die pipeline_cpu_pipelined $?
 step "receive side"
 timeout -k 10 180 python tools/bench_rx.py > $O/rx_timing.json || die rx $?
 cat $O/rx_timing.json

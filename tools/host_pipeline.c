@@ -22,8 +22,9 @@
  * Build: gcc -O2 -pthread -Iinclude -o tools/host_pipeline tools/host_pipeline.c \
  *          -Lwireguard-java_amd -l:libwgaead.so -ldl -Wl,-rpath,'$ORIGIN/../wireguard-java_amd'
  * Run:   tools/host_pipeline [--backend gpu|cpu] [--oracle PATH] [--threads T] [--packets N]
- *                            [--len L] [--reps R] [--udp-streams K] [--tun]
- *        (--tun: try a real tun device; K socket pairs with a sender and a receiver thread each)
+ *                            [--len L] [--reps R] [--udp-streams K] [--chunks C] [--tun]
+ *        (--tun: try a real tun device; K socket pairs with a sender and a receiver thread each;
+ *         --chunks C > 1: seal, UDP and open overlap chunk by chunk, see "pipelined mode" below)
  * Output: one JSON line. */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
@@ -34,6 +35,7 @@
 #include <linux/if_tun.h>
 #include <netinet/in.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdatomic.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -236,11 +238,145 @@ static void* tx_loop(void* arg) {
   return NULL;
 }
 
+/* ---- pipelined mode (--chunks C > 1): seal, UDP and open overlap chunk by chunk --------------
+ * The batch is cut into C chunks; the main thread seals chunk c+1 while the senders send chunk c and
+ * an opener thread opens every chunk the receivers have completely received, as a tun reader, the
+ * UDP workers and the peer's receive side would run at once. Stripe k of K sends, from every chunk,
+ * the packets [c cs + k cs/K, c cs + (k+1) cs/K); its receiver places the i-th datagram it gets at
+ * the position of the stripe's i-th packet (loopback UDP keeps a socket's order). */
+typedef struct {
+  stripe_t* S;
+  int k, K;
+  uint32_t n, cs, C;
+  _Atomic uint32_t* sealed; /* chunks sealed so far */
+} ptx_t;
+
+static uint32_t ppos(uint32_t i, int k, int K, uint32_t cs) { /* the stripe's i-th packet */
+  const uint32_t m = cs / (uint32_t)K;
+  return (i / m) * cs + (uint32_t)k * m + i % m;
+}
+
+typedef struct {
+  rx_t* R;
+  int k, K;
+  uint32_t cs;
+  uint8_t* base; /* the whole received ring */
+  uint32_t* lens;
+} prx_t;
+
+static void* prx_loop(void* arg) {
+  prx_t* P = (prx_t*)arg;
+  rx_t* r = P->R;
+  struct mmsghdr msgs[256];
+  struct iovec iov[256];
+  while (!atomic_load(&r->stop)) {
+    uint32_t have = atomic_load(&r->received);
+    if (have >= r->n) break;
+    uint32_t want = r->n - have < 256 ? r->n - have : 256;
+    for (uint32_t j = 0; j < want; ++j) {
+      iov[j].iov_base = P->base + (size_t)ppos(have + j, P->k, P->K, P->cs) * UDP_STRIDE;
+      iov[j].iov_len = UDP_STRIDE;
+      memset(&msgs[j].msg_hdr, 0, sizeof msgs[j].msg_hdr);
+      msgs[j].msg_hdr.msg_iov = &iov[j];
+      msgs[j].msg_hdr.msg_iovlen = 1;
+    }
+    struct timespec to = {0, 20 * 1000 * 1000};
+    int got = recvmmsg(r->sock, msgs, want, MSG_WAITFORONE, &to);
+    if (got <= 0) continue;
+    for (int j = 0; j < got; ++j) P->lens[ppos(have + (uint32_t)j, P->k, P->K, P->cs)] = msgs[j].msg_len;
+    atomic_store(&r->received, have + (uint32_t)got);
+  }
+  return NULL;
+}
+
+static void* ptx_loop(void* arg) {
+  ptx_t* T = (ptx_t*)arg;
+  stripe_t* S = T->S;
+  struct mmsghdr msgs[256];
+  struct iovec iov[256];
+  const uint32_t total = T->n / (uint32_t)T->K, m = T->cs / (uint32_t)T->K;
+  uint32_t sent = 0;
+  double last_progress = now_s();
+  while (sent < total) {
+    const uint32_t ready = atomic_load(T->sealed) * m;  /* the stripe's packets sealed so far */
+    const uint32_t inflight = sent - atomic_load(&S->R.received);
+    if (sent >= ready || inflight + 256 > S->window) {
+      if (now_s() - last_progress > 1.0) break; /* sealer or receiver stalled */
+      sched_yield();                             /* the CPUs belong to the crypto and the sockets */
+      continue;
+    }
+    last_progress = now_s();
+    uint32_t k = ready - sent < 256 ? ready - sent : 256;
+    for (uint32_t j = 0; j < k; ++j) {
+      iov[j].iov_base = S->tx + (size_t)ppos(sent + j, T->k, T->K, T->cs) * UDP_STRIDE;
+      iov[j].iov_len = HDR + S->L + 16;
+      memset(&msgs[j].msg_hdr, 0, sizeof msgs[j].msg_hdr);
+      msgs[j].msg_hdr.msg_iov = &iov[j];
+      msgs[j].msg_hdr.msg_iovlen = 1;
+      msgs[j].msg_hdr.msg_name = &S->addr;
+      msgs[j].msg_hdr.msg_namelen = sizeof S->addr;
+    }
+    const int got = sendmmsg(S->tx_sock, msgs, k, 0);
+    if (got > 0) sent += (uint32_t)got;
+  }
+  S->sent = sent;
+  return NULL;
+}
+
+typedef struct {
+  backend* B;
+  stripe_t* SS;
+  int K;
+  uint32_t n, cs, C, L;
+  uint64_t ctr;
+  uint8_t *rxr, *back;
+  uint32_t* lens;
+  wg_pkt* od;
+  uint32_t* st;
+  double t_open;    /* time inside do_open */
+  uint32_t opened;  /* packets opened */
+  int failed;
+} popen_t;
+
+static void* popen_loop(void* arg) {
+  popen_t* O = (popen_t*)arg;
+  const uint32_t m = O->cs / (uint32_t)O->K;
+  for (uint32_t c = 0; c < O->C; ++c) {
+    const double w0 = now_s();
+    for (int k = 0; k < O->K; ++k)  /* every stripe's share of chunk c has arrived */
+      while (atomic_load(&O->SS[k].R.received) < (c + 1) * m) {
+        if (now_s() - w0 > 2.0) return NULL; /* dropped datagrams: the chunk never completes */
+        sched_yield();
+      }
+    uint32_t got = 0;
+    for (uint32_t i = 0; i < O->cs; ++i) {
+      const uint32_t pos = c * O->cs + i;
+      const uint8_t* h = O->rxr + (size_t)pos * UDP_STRIDE;
+      uint64_t cc;
+      memcpy(&cc, h + 8, 8);
+      const uint32_t idx = (uint32_t)(cc - O->ctr);
+      O->od[pos] = (wg_pkt){(uint64_t)pos * UDP_STRIDE + HDR, (uint64_t)(idx < O->n ? idx : 0) * TUN_STRIDE, cc,
+                            O->lens[pos] >= HDR + 16 ? O->lens[pos] - HDR - 16 : 0, 0};
+      ++got;
+    }
+    const double a = now_s();
+    if (do_open(O->B, O->od + (size_t)c * O->cs, got, O->rxr, (uint64_t)O->n * UDP_STRIDE, O->back,
+                (uint64_t)O->n * TUN_STRIDE, O->st + (size_t)c * O->cs, O->L) != 0) {
+      O->failed = 1;
+      return NULL;
+    }
+    O->t_open += now_s() - a;
+    O->opened += got;
+  }
+  return NULL;
+}
+
 int main(int argc, char** argv) {
   const char* bk = "gpu";
   const char* oracle_path = NULL;
   uint32_t n = 65536, L = 1420, reps = 5;
   int threads = 16, try_tun = 0, streams = 1;
+  uint32_t chunks = 1;
   for (int i = 1; i < argc; ++i)
     if (!strcmp(argv[i], "--tun")) try_tun = 1;
   for (int i = 1; i + 1 < argc; i += 2) {
@@ -252,6 +388,11 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--len")) L = (uint32_t)atoi(argv[i + 1]);
     else if (!strcmp(argv[i], "--reps")) reps = (uint32_t)atoi(argv[i + 1]);
     else if (!strcmp(argv[i], "--udp-streams")) streams = atoi(argv[i + 1]);
+    else if (!strcmp(argv[i], "--chunks")) chunks = (uint32_t)atoi(argv[i + 1]);
+  }
+  if (chunks < 1 || n % chunks || (n / chunks) % (uint32_t)(streams > 0 ? streams : 1)) {
+    fprintf(stderr, "--chunks must divide --packets into chunks that --udp-streams divides\n");
+    return 2;
   }
   if (L < 28 || L > 1420 || n == 0 || reps == 0 || streams < 1 || streams > 64) {
     fprintf(stderr, "bad arguments\n");
@@ -327,7 +468,70 @@ int main(int argc, char** argv) {
   double t_seal = 0, t_xfer = 0, t_open = 0, t_total = 0;
   uint64_t delivered = 0, dropped = 0, bad = 0, mismatched = 0;
   uint64_t ctr = 0;
-  for (uint32_t rep = 0; rep <= reps; ++rep) { /* rep 0: warm-up */
+  const uint32_t cs = n / chunks;
+  for (uint32_t rep = 0; chunks > 1 && rep <= reps; ++rep) { /* pipelined; rep 0: warm-up */
+    _Atomic uint32_t sealed = 0;
+    pthread_t rth[64], tth[64], oth;
+    prx_t PR[64];
+    ptx_t PT[64];
+    popen_t O = {&B, SS, streams, n, cs, chunks, L, ctr, rxr, back, lens, od, st, 0.0, 0u, 0};
+    memset(lens, 0, sizeof(uint32_t) * n);
+    const double a = now_s();
+    for (int k = 0; k < streams; ++k) {
+      stripe_t* S = &SS[k];
+      S->R.n = n / (uint32_t)streams;
+      atomic_store(&S->R.received, 0);
+      atomic_store(&S->R.stop, 0);
+      PR[k] = (prx_t){&S->R, k, streams, cs, rxr, lens};
+      PT[k] = (ptx_t){S, k, streams, n, cs, chunks, &sealed};
+      pthread_create(&rth[k], NULL, prx_loop, &PR[k]);
+      pthread_create(&tth[k], NULL, ptx_loop, &PT[k]);
+    }
+    pthread_create(&oth, NULL, popen_loop, &O);
+    double ts = 0;
+    for (uint32_t c = 0; c < chunks; ++c) {
+      for (uint32_t i = c * cs; i < (c + 1) * cs; ++i) {
+        uint8_t* h = tx + (size_t)i * UDP_STRIDE;
+        const uint32_t type = 4, rcv = 0x01020304u;
+        const uint64_t cc = ctr + i;
+        memcpy(h, &type, 4); memcpy(h + 4, &rcv, 4); memcpy(h + 8, &cc, 8);
+        sd[i] = (wg_pkt){(uint64_t)i * TUN_STRIDE, (uint64_t)i * UDP_STRIDE + HDR, cc, L, 0};
+      }
+      const double s0 = now_s();
+      if (do_seal(&B, sd + (size_t)c * cs, cs, tun, (uint64_t)n * TUN_STRIDE, tx, (uint64_t)n * UDP_STRIDE, L) != 0) {
+        fprintf(stderr, "seal failed: %s\n", B.gpu ? wg_last_error() : "");
+        return 1;
+      }
+      ts += now_s() - s0;
+      atomic_store(&sealed, c + 1);
+    }
+    for (int k = 0; k < streams; ++k) pthread_join(tth[k], NULL);
+    pthread_join(oth, NULL);
+    for (int k = 0; k < streams; ++k) {
+      atomic_store(&SS[k].R.stop, 1);
+      pthread_join(rth[k], NULL);
+    }
+    const double d = now_s();
+    if (O.failed) {
+      fprintf(stderr, "open failed: %s\n", B.gpu ? wg_last_error() : "");
+      return 1;
+    }
+    if (rep > 0) {
+      t_seal += ts;
+      t_open += O.t_open;
+      t_total += d - a;
+      t_xfer += d - a;  /* the sockets run the whole time */
+      delivered += O.opened;
+      dropped += n - O.opened;
+      for (uint32_t i = 0; i < O.opened; ++i) {
+        if (st[i]) { ++bad; continue; }
+        const uint32_t idx = (uint32_t)(od[i].counter - ctr);
+        if (memcmp(back + (size_t)idx * TUN_STRIDE, tun + (size_t)idx * TUN_STRIDE, L)) ++mismatched;
+      }
+    }
+    ctr += n;
+  }
+  for (uint32_t rep = 0; chunks == 1 && rep <= reps; ++rep) { /* rep 0: warm-up */
     const double a = now_s();
     for (uint32_t i = 0; i < n; ++i) {
       uint8_t* h = tx + (size_t)i * UDP_STRIDE;
@@ -396,12 +600,12 @@ int main(int argc, char** argv) {
     ctr += n;
   }
   const double GiB = (double)(1u << 30), per = (double)n * L;
-  printf("{\"tool\": \"host_pipeline\", \"backend\": \"%s\", \"threads\": %d, \"packets\": %u, \"len\": %u, "
+  printf("{\"tool\": \"host_pipeline\", \"mode\": \"%s\", \"chunks\": %u, \"backend\": \"%s\", \"threads\": %d, \"packets\": %u, \"len\": %u, "
          "\"reps\": %u, \"udp_streams\": %d, \"tun\": \"%s\", \"tun_read_gib_s\": %.3f, \"udp_rcvbuf\": %d, \"inflight_window\": %u, "
          "\"seal_gib_s\": %.3f, \"udp_loopback_gib_s\": %.3f, \"open_gib_s\": %.3f, "
          "\"end_to_end_gib_s\": %.3f, \"delivered\": %llu, \"dropped\": %llu, \"bad_tag\": %llu, "
          "\"mismatched\": %llu}\n",
-         bk, B.gpu ? 0 : threads, n, L, reps, streams, g_tun_note, tun_rate, rcvbuf, window, per * reps / t_seal / GiB,
+         chunks > 1 ? "pipelined" : "stages in turn", chunks, bk, B.gpu ? 0 : threads, n, L, reps, streams, g_tun_note, tun_rate, rcvbuf, window, per * reps / t_seal / GiB,
          (double)delivered * L / t_xfer / GiB, (double)delivered * L / t_open / GiB,
          (double)delivered * L / t_total / GiB, (unsigned long long)delivered, (unsigned long long)dropped,
          (unsigned long long)bad, (unsigned long long)mismatched);
