@@ -128,7 +128,7 @@ struct wg_ctx {
   // host-API staging
   DevBuf h_desc, h_in, h_out, h_aad, h_status, h_keys;
   std::mutex mu;  // serialises host-API calls and plan workspace reuse
-  PPServer* pp = nullptr;  // persistent per-packet server (wg_seal1 / wg_open1)
+  std::atomic<PPServer*> pp{nullptr};  // persistent per-packet server (wg_seal1 / wg_open1), made once
   std::mutex pp_mu;
   // Host mirror of the key table, read by the paths that send a key WITH the packet (the per-packet
   // server, the asynchronous queue): 4 words per slot behind a per-slot sequence lock, so readers

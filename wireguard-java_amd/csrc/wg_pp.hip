@@ -554,13 +554,25 @@ struct PPServer {
   uint32_t* d_exited = nullptr;  // device: {exited, quit} then the 8-B last-activity stamp
   std::unique_ptr<std::atomic<uint32_t>[]> state;  // per entry: kFree / kBusy / kOrphan
   std::unique_ptr<std::atomic<uint64_t>[]> pub;    // per entry: seq of its last publication
-  std::atomic<uint64_t> calls{0};                  // call numbers (seq = call + 1)
+  std::atomic<uint64_t> calls{0};                  // call numbers (WG_PP_STAMPS builds: seq = call + 1)
   std::atomic<uint32_t> threads{0};                // calling threads seen (each takes the next wave)
   std::mutex launch_mu;
   std::atomic<uint64_t> running{0};  // gen of the launched kernel (0: none yet)
   uint64_t gen = 0;                  // guarded by launch_mu
   uint32_t waves = 16, idle_us = 20000, life_ms = 250;
-  std::atomic<uint64_t> launches{0}, packets{0};
+  std::atomic<uint64_t> launches{0};
+  // packets served, one counter per group of units (wg_batcher_stats sums them): callers of different
+  // units do not write one shared line per call
+  static constexpr uint32_t kShards = 16;
+  struct alignas(64) Shard {
+    std::atomic<uint64_t> n{0};
+  };
+  Shard served[kShards];
+  uint64_t packets() const {
+    uint64_t t = 0;
+    for (const Shard& x : served) t += x.n.load(std::memory_order_relaxed);
+    return t;
+  }
   int fail_launches = 0;  // test hook (WG_PP_TEST_FAIL_LAUNCHES): refuse this many launches
   uint32_t spin_limit = 4096;     // polls of the completion word before a waiting caller sleeps (WG_PP_SPIN)
   // more calls in flight than this: 64 polls, then sleep (WG_PP_SPIN_CALLERS). Default: the CPUs the
@@ -606,9 +618,15 @@ void pp_free(PPServer* S) {
 }
 
 int pp_get(wg_ctx* c, PPServer** out) {
+  // the server exists after the context's first per-packet call: no lock after that (a mutex taken by
+  // every call of 16 callers made them queue on it)
+  if (PPServer* S = c->pp.load(std::memory_order_acquire)) {
+    *out = S;
+    return WG_OK;
+  }
   std::lock_guard<std::mutex> lk(c->pp_mu);
-  if (c->pp) {
-    *out = c->pp;
+  if (PPServer* S = c->pp.load(std::memory_order_relaxed)) {
+    *out = S;
     return WG_OK;
   }
   DeviceGuard g(c->device);
@@ -648,7 +666,7 @@ int pp_get(wg_ctx* c, PPServer** out) {
     delete S;
     return fail(WG_ENOMEM, "per-packet server: pinned ring or device state could not be allocated");
   }
-  c->pp = S;
+  c->pp.store(S, std::memory_order_release);
   *out = S;
   return WG_OK;
 }
@@ -695,8 +713,8 @@ void pp_stop(wg_ctx* c) {
   PPServer* S = nullptr;
   {
     std::lock_guard<std::mutex> lk(c->pp_mu);
-    S = c->pp;
-    c->pp = nullptr;
+    S = c->pp.load(std::memory_order_relaxed);
+    c->pp.store(nullptr, std::memory_order_relaxed);
   }
   if (!S) return;
   DeviceGuard g(c->device);
@@ -867,15 +885,21 @@ int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const u
   if (stamp) st.t_enter = pp_now_ns();
   uint32_t key[8];
   key_snapshot(c, key_slot, key);
-  const uint64_t k = S->calls.fetch_add(1, std::memory_order_relaxed);
-  const uint64_t seq = k + 1;  // unique per call: the completion word echoes it
   if (t_pp.server != (const void*)S) {
     t_pp.server = S;
     t_pp.wave = S->threads.fetch_add(1, std::memory_order_relaxed);
     t_pp.n = 0;
   }
   const uint32_t W = S->waves, E = wgpp::kRing / W;
-  const uint32_t i = pp_claim(S, (t_pp.wave % W) * E + (t_pp.n++ % E), k);
+  const uint32_t i = pp_claim(S, (t_pp.wave % W) * E + (t_pp.n++ % E), t_pp.n);
+  // the completion word echoes seq: it must differ from every earlier publication of this entry, so the
+  // entry's own count will do and callers share no counter (one shared line that 16 callers increment per
+  // call cost each of them a cross-core transfer); tools/pp_stamps indexes its stamps by call number
+#ifdef WG_PP_STAMPS
+  const uint64_t seq = S->calls.fetch_add(1, std::memory_order_relaxed) + 1;
+#else
+  const uint64_t seq = S->pub[i].load(std::memory_order_relaxed) + 1;
+#endif
   if (stamp) st.t_claimed = pp_now_ns();
   const uint64_t launches0 = S->launches.load(std::memory_order_relaxed);
   wgpp::Hdr* h = (wgpp::Hdr*)S->in_slot(i);
@@ -928,7 +952,7 @@ int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const u
     } else {
       result = status == WG_PKT_BADTAG ? 1 : fail(WG_EDEVICE, "per-packet server refused the packet");
     }
-    S->packets.fetch_add(1, std::memory_order_relaxed);
+    S->served[t_pp.wave % PPServer::kShards].n.fetch_add(1, std::memory_order_relaxed);
     memset(h->key, 0, 32);  // no key material left in the ring
     S->state[i].store(kFree, std::memory_order_release);
   } else {
@@ -1010,9 +1034,9 @@ int wg_batcher_stats(wg_ctx* c, uint64_t* launches, uint64_t* packets) {
   uint64_t l = 0, p = 0;
   {
     std::lock_guard<std::mutex> lk(c->pp_mu);
-    if (c->pp) {
-      l = c->pp->launches.load();
-      p = c->pp->packets.load();
+    if (PPServer* S = c->pp.load()) {
+      l = S->launches.load();
+      p = S->packets();
     }
   }
   if (launches) *launches = l;
