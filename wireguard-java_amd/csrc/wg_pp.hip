@@ -414,7 +414,10 @@ __device__ __forceinline__ uint64_t lane_u64(uint64_t v, uint32_t k) {
 // One doorbell poll in flight per unit. Two or four in flight (staggered) found a publication sooner
 // but congested the device's PCIe reads: the payload read after the doorbell took 1.9-3.5 (two) and
 // 6.3 us (four) instead of 1.4, and a one-caller call 8-17 us instead of 7.7
-// (profiles/r05_pp_poll_ab.jsonl).
+// (profiles/r05_pp_poll_ab.jsonl). Only the first two polls after a service overlap, the second
+// kPostServeStagger x 64 cycles behind: 1 caller p50 7.7 -> 6.8-7.0 us, 16 callers 2.4-2.6 -> 2.6-2.7
+// GiB/s (20, 26, 34, 44: profiles/r05_pp_stagger_ab.jsonl).
+constexpr uint32_t kPostServeStagger = 26;
 __global__ void __launch_bounds__(kUnitThreads) k_pp(PPParams P) {
   __shared__ Unit U;
   const uint32_t w = blockIdx.x;
@@ -470,8 +473,15 @@ __global__ void __launch_bounds__(kUnitThreads) k_pp(PPParams P) {
           }
           return 0;
         };
-        int act;
-        for (uint32_t backoff = 0;;) {  // one poll at a time, at most 2 x 256 cycles apart
+        int act = 0;
+        {  // right after a service (when a caller's next packet is likeliest): a second poll about half
+           // a round trip behind the first, then one at a time
+          const uint64_t v1 = __hip_atomic_load(paddr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __builtin_amdgcn_s_sleep(kPostServeStagger);
+          const uint64_t v2 = __hip_atomic_load(paddr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          if ((act = look(v1)) == 0) act = look(v2);
+        }
+        for (uint32_t backoff = 0; act == 0;) {  // one poll at a time, at most 2 x 256 cycles apart
           const uint64_t v = __hip_atomic_load(paddr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if ((act = look(v)) != 0) break;
           if (backoff < 2u) ++backoff;
