@@ -1,6 +1,6 @@
 #!/bin/bash
 # tools/batcher_bench for build_ab/<V>/ builds, alternating on one box (1, 8, 16 callers), after the
-# batcher tests of the in-tree build: usage r05_bbab.sh OUT V1 V2 ...
+# batcher tests of the in-tree build: usage pp_ab.sh OUT V1 V2 ...
 set -o pipefail
 O=gpurun_out/$1; shift; mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_batcher.py tests/test_keypair.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -20 $O/tests.log; exit 1; }

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Per-packet server, final in-tree build: batcher tests, stage stamps, callers 1..32
+# Per-packet server, in-tree build: batcher tests, stage stamps, then 1..64 callers (tools/batcher_bench)
+# Usage: bash tools/pp_round.sh OUT
 set -o pipefail
 O=gpurun_out/${1:-r05ppf2}; mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_batcher.py tests/test_keypair.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -20 $O/tests.log; exit 1; }

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Per-packet server build variants under build_ab/<V>/ (libwgaead.so + batcher_bench + pp_stamps),
-# alternating on one box: usage r05_ppv.sh OUT V1 V2 ...
+# alternating on one box: usage pp_variants.sh OUT V1 V2 ...
 set -o pipefail
 O=gpurun_out/$1; shift; mkdir -p $O
 for v in "$@"; do
