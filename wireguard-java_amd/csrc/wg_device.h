@@ -220,7 +220,12 @@ __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
   asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(d), "=s"(cc) : "v"(a), "v"(b), "v"(c));
   return d;
 }
+// The same product visible to the compiler. Between two dependent asm statements the hazard
+// recognizer inserts an s_nop 0 (it cannot see into them); other waves on the SIMD hide those in the
+// transport kernels, a wave on its own pays them (the per-packet server's Poly1305 wave, wg_pp.hip).
+__device__ __forceinline__ uint64_t mad64c(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
 #ifdef WG_POLY_C  // the plain-C product (the compiler adds each limb's carry with a separate 64-bit add)
+template <bool ASM = true>
 __device__ __forceinline__ void poly_mul(uint32_t h[5], const uint32_t r[5], const uint32_t s[5]) {
   const uint32_t h0 = h[0], h1 = h[1], h2 = h[2], h3 = h[3], h4 = h[4];
   uint64_t d = (uint64_t)h0 * r[0] + (uint64_t)h1 * s[4] + (uint64_t)h2 * s[3] + (uint64_t)h3 * s[2] +
@@ -247,18 +252,20 @@ __device__ __forceinline__ void poly_mul(uint32_t h[5], const uint32_t r[5], con
 // Default: each v_mad_u64_u32 as an asm statement, so every limb's chain starts from the
 // previous limb's carry instead of the compiler adding the carry to a separately formed
 // chain: -1.4% VALU instructions per k_transport launch (SQ_INSTS_VALU 37.70 M -> 37.18 M on
-// C1), bit-exact.
+// C1), bit-exact. ASM = false: the same chains with compiler-visible products (mad64c).
+template <bool ASM = true>
 __device__ __forceinline__ void poly_mul(uint32_t h[5], const uint32_t r[5], const uint32_t s[5]) {
+  auto mad = [](uint32_t a, uint32_t b, uint64_t c) { return ASM ? mad64(a, b, c) : mad64c(a, b, c); };
   const uint32_t h0 = h[0], h1 = h[1], h2 = h[2], h3 = h[3], h4 = h[4];
-  uint64_t d = mad64(h0, r[0], mad64(h1, s[4], mad64(h2, s[3], mad64(h3, s[2], (uint64_t)h4 * s[1]))));
+  uint64_t d = mad(h0, r[0], mad(h1, s[4], mad(h2, s[3], mad(h3, s[2], (uint64_t)h4 * s[1]))));
   h[0] = (uint32_t)d & M26;
-  d = mad64(h4, s[2], mad64(h3, s[3], mad64(h2, s[4], mad64(h1, r[0], mad64(h0, r[1], d >> 26)))));
+  d = mad(h4, s[2], mad(h3, s[3], mad(h2, s[4], mad(h1, r[0], mad(h0, r[1], d >> 26)))));
   h[1] = (uint32_t)d & M26;
-  d = mad64(h4, s[3], mad64(h3, s[4], mad64(h2, r[0], mad64(h1, r[1], mad64(h0, r[2], d >> 26)))));
+  d = mad(h4, s[3], mad(h3, s[4], mad(h2, r[0], mad(h1, r[1], mad(h0, r[2], d >> 26)))));
   h[2] = (uint32_t)d & M26;
-  d = mad64(h4, s[4], mad64(h3, r[0], mad64(h2, r[1], mad64(h1, r[2], mad64(h0, r[3], d >> 26)))));
+  d = mad(h4, s[4], mad(h3, r[0], mad(h2, r[1], mad(h1, r[2], mad(h0, r[3], d >> 26)))));
   h[3] = (uint32_t)d & M26;
-  d = mad64(h4, r[0], mad64(h3, r[1], mad64(h2, r[2], mad64(h1, r[3], mad64(h0, r[4], d >> 26)))));
+  d = mad(h4, r[0], mad(h3, r[1], mad(h2, r[2], mad(h1, r[3], mad(h0, r[4], d >> 26)))));
   h[4] = (uint32_t)d & M26;
   uint32_t c = (uint32_t)(d >> 26);
   h[0] += c * 5u;

@@ -165,7 +165,7 @@ __device__ __forceinline__ void pow_scan_step(uint32_t y[5], bool take) {
     t[i] = y[i];
   }
   poly_scale5(z, zs);
-  poly_mul(t, z, zs);
+  poly_mul<false>(t, z, zs);  // a lone wave: no s_nop between the products (wg_device.h)
 #pragma unroll
   for (int i = 0; i < 5; ++i) y[i] = take ? t[i] : y[i];
 }
@@ -193,7 +193,7 @@ __device__ __forceinline__ void mac_tag(const uint4* mac, uint32_t len, uint32_t
   const uint32_t D = 64u * T - M;
   uint32_t acc[5] = {0, 0, 0, 0, 0};
   for (uint32_t t = 0; t < T; ++t) {
-    if (t) poly_mul(acc, R, Rs);
+    if (t) poly_mul<false>(acc, R, Rs);
     const uint32_t p = 64u * t + 63u - lane;
     if (p >= D) {
       const uint32_t c = p - D;
@@ -205,7 +205,7 @@ __device__ __forceinline__ void mac_tag(const uint4* mac, uint32_t len, uint32_t
       for (int i = 0; i < 5; ++i) acc[i] += cl[i];
     }
   }
-  poly_mul(acc, y, ys);
+  poly_mul<false>(acc, y, ys);
   // sum over the wave: each row of 16 (limbs stay < 2^31), carry, then the four row sums
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
