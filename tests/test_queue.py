@@ -334,7 +334,8 @@ def test_batched_submits_bit_exact_beside_single_submits():
     runs of 1..300 (more than a lane's share of the 1,024-slot ring, so runs span several free-slot
     runs and wait for the consumer), a fourth submits one at a time; every sealed packet matches the
     oracle, then the forwarder shape: reaped completions submitted to an open queue in batches of
-    what one wg_reap returned, every plaintext equal to the input."""
+    what one wg_reap returned (every 50th with a forged tag: WG_PKT_BADTAG, no data), every other
+    plaintext equal to the input."""
     W = wg()
     eng = W.Engine(0, key_slots=8)
     qs = qo = None
@@ -390,9 +391,17 @@ def test_batched_submits_bit_exact_beside_single_submits():
             for user, ctr, st, data in done:
                 assert st == 0, st
                 sealed[user] = (ctr, data)
-            # forward what this reap returned to the open queue in one call
+            # forward what this reap returned to the open queue in one call, every 50th with a
+            # flipped tag bit
             if done:
-                assert qo.submit_n([(sent[u][0], c, d, u) for u, c, _, d in done]) == len(done)
+                fwd = []
+                for u, c, _, d in done:
+                    if (u & 0xffffffff) % 50 == 7:
+                        d = bytearray(d)
+                        d[-1 - (u % 16)] ^= 0x20
+                        d = bytes(d)
+                    fwd.append((sent[u][0], c, d, u))
+                assert qo.submit_n(fwd) == len(done)
         for x in th:
             x.join()
         for user, (slot, ctr, pt) in sent.items():
@@ -403,7 +412,10 @@ def test_batched_submits_bit_exact_beside_single_submits():
         assert not errors, errors[:3]
         assert len(got) == T * N, (len(got), qo.stats())
         for user, (slot, ctr, pt) in sent.items():
-            assert got[user] == (ctr, 0, pt), user
+            if (user & 0xffffffff) % 50 == 7:
+                assert got[user] == (ctr, W._lib.WG_PKT_BADTAG, None), user
+            else:
+                assert got[user] == (ctr, 0, pt), user
     finally:
         for q in (qs, qo):
             if q is not None:
