@@ -7,7 +7,7 @@ timeout -k 10 300 python -u -m pytest tests/test_batcher.py tests/test_keypair.p
 tail -1 $O/tests.log
 for a in "1420" "1420 alt" "64" "4000"; do timeout -k 10 60 ./tools/pp_stamps $a >> $O/stamps.jsonl || { echo "stamps rc $?"; exit 1; }; done
 for r in 1 2; do
-  for t in 1 2 4 8 12 16 24 32 64; do
+  for t in 1 2 4 8 12 16 24 32 64 128; do
     timeout -k 10 120 ./tools/batcher_bench $t $((t == 1 ? 4000 : 160000 / t)) 1420 >> $O/callers.jsonl || { echo "rc $?"; exit 1; }
   done
 done

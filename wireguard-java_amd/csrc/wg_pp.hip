@@ -594,7 +594,12 @@ struct PPServer {
   std::unique_ptr<std::atomic<uint32_t>[]> wake, waiting;
   std::atomic<uint32_t> sleepers{0};
   std::atomic<bool> waker_started{false};
-  std::thread waker;
+  // waker threads (entry i served by waker i % count): one spends a futex wake (a syscall) per sleeping
+  // caller's completion and capped the callers past the CPU count at about 1.2 GiB/s; four reached
+  // 1.9-2.7 GiB/s for 24-128 callers with no quota throttling (profiles/r05_pp_wakers_ab.jsonl).
+  // Default: a quarter of the CPUs the process may use, 1..4 (WG_PP_WAKERS overrides, 1..16)
+  std::vector<std::thread> wakers;
+  uint32_t n_wakers = 1;
   std::atomic<bool> waker_quit{false};
   std::mutex wmu;
   std::condition_variable wcv;
@@ -653,6 +658,8 @@ int pp_get(wg_ctx* c, PPServer** out) {
   if (const char* e = getenv("WG_PP_TEST_HOLD_US")) S->hold_us = (uint32_t)atoi(e);
   if (const char* e = getenv("WG_PP_SPIN")) S->spin_limit = (uint32_t)std::max(1, atoi(e));
   if (const char* e = getenv("WG_PP_CALL_STAMPS")) S->stamps = atoi(e) != 0;
+  S->n_wakers = std::min(4u, std::max(1u, host_cpus() / 4u));
+  if (const char* e = getenv("WG_PP_WAKERS")) S->n_wakers = (uint32_t)std::min(16, std::max(1, atoi(e)));
   S->spin_callers = host_cpus();
   if (const char* e = getenv("WG_PP_SPIN_CALLERS")) S->spin_callers = (uint32_t)std::max(0, atoi(e));
   S->wake.reset(new std::atomic<uint32_t>[wgpp::kRing]);
@@ -733,7 +740,8 @@ void pp_stop(wg_ctx* c) {
     S->waker_quit.store(true);
     S->wcv.notify_all();
   }
-  if (S->waker.joinable()) S->waker.join();
+  for (std::thread& w : S->wakers)
+    if (w.joinable()) w.join();
   S->ctl()->stop = 1;  // every wave sees it at its next poll and exits
   (void)hipStreamSynchronize(S->stream);
   pp_free(S);
@@ -816,12 +824,14 @@ long futex(std::atomic<uint32_t>* w, int op, uint32_t val, const struct timespec
   return syscall(SYS_futex, (uint32_t*)w, op, val, t, nullptr, 0);
 }
 
-// The waker: while callers sleep (pp_sleep), one host thread polls their completion words and wakes
-// each caller whose result has landed (a futex per entry), and relaunches the server if it left.
+// The wakers: while callers sleep (pp_sleep), n_wakers host threads poll their completion words (waker
+// k the entries i with i % n_wakers == k) and wake each caller whose result has landed (a futex per
+// entry); waker 0 also relaunches the server if it left.
 // Sleeping callers burn no CPU: 64 or 128 callers spinning on 16 cores exhaust a CPU quota early in
 // its period and are then all throttled until the next one (p999 ~70-90 ms).
-void pp_waker(PPServer* S) {
+void pp_waker(PPServer* S, uint32_t k0) {
   uint32_t iter = 0;
+  const uint32_t nw = S->n_wakers;
   while (!S->waker_quit.load(std::memory_order_acquire)) {
     if (S->sleepers.load(std::memory_order_acquire) == 0) {
       std::unique_lock<std::mutex> lk(S->wmu);
@@ -830,13 +840,13 @@ void pp_waker(PPServer* S) {
       });
       continue;
     }
-    for (uint32_t i = 0; i < wgpp::kRing; ++i) {
+    for (uint32_t i = k0; i < wgpp::kRing; i += nw) {
       if (!S->waiting[i].load(std::memory_order_acquire)) continue;
       const uint64_t d = __atomic_load_n((const uint64_t*)S->done(i), __ATOMIC_ACQUIRE);
       if ((d >> 8) == S->pub[i].load(std::memory_order_relaxed) && !S->wake[i].exchange(1))
         futex(&S->wake[i], FUTEX_WAKE_PRIVATE, 1, nullptr);
     }
-    if ((++iter & 63u) == 0) (void)pp_ensure(S);  // a server that left while callers sleep
+    if ((++iter & 63u) == 0 && k0 == 0) (void)pp_ensure(S);  // a server that left while callers sleep
     for (int k = 0; k < 32; ++k) __builtin_ia32_pause();
   }
 }
@@ -848,13 +858,14 @@ int pp_sleep(PPServer* S, uint32_t i, uint64_t seq, uint64_t* d_out) {
   // 128 callers taking it for every sleep, the lock itself burnt the CPU quota
   if (!S->waker_started.load(std::memory_order_acquire)) {
     std::lock_guard<std::mutex> lk(S->wmu);
-    if (!S->waker.joinable()) S->waker = std::thread(pp_waker, S);
+    if (S->wakers.empty())
+      for (uint32_t k = 0; k < S->n_wakers; ++k) S->wakers.emplace_back(pp_waker, S, k);
     S->waker_started.store(true, std::memory_order_release);
   }
   S->waiting[i].store(1, std::memory_order_seq_cst);
   if (S->sleepers.fetch_add(1, std::memory_order_seq_cst) == 0) {
     std::lock_guard<std::mutex> lk(S->wmu);
-    S->wcv.notify_one();
+    S->wcv.notify_all();
   }
   int rc = WG_OK;
   const struct timespec to = {0, 2 * 1000 * 1000};
