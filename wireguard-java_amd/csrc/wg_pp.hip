@@ -797,7 +797,7 @@ uint32_t pp_claim(PPServer* S, uint32_t start, uint64_t k) {
         nb += st == kBusy;
         no += st == kOrphan;
       }
-      fprintf(stderr, "[wg_pp] claim of call %llu finds no free entry: free %u busy %u orphan %u\n",
+      fprintf(stderr, "[wg_pp] call %llu of this thread finds no free entry: free %u busy %u orphan %u\n",
               (unsigned long long)k, nf, nb, no);
     }
     // more calls in flight than entries: wait for one to finish
