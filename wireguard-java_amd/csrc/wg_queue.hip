@@ -227,6 +227,7 @@ struct wg_queue {
   alignas(64) std::atomic<uint32_t> freed_acc{0};
   uint32_t wake_batch = 256;
   bool steal = true;  // a producer whose lane has no free slot takes one from another lane (WG_QUEUE_STEAL=0: no)
+  uint32_t prefetch = 2;  // wg_submit_*_n: packets ahead whose bytes are prefetched (WG_QUEUE_PREFETCH)
   std::vector<wgq::Batch> batches;  // `inflight` launch buffers, used round robin
   DevBuf lpt_hist, lpt_order;       // the queue's own longest-first workspace (its own stream)
   hipStream_t stream = nullptr;
@@ -553,6 +554,13 @@ int queue_submit_n(wg_queue* q, int mode, const wg_submit* p, uint32_t n) {
     uint64_t rt = ln.r_tail.load(std::memory_order_relaxed);
     const uint64_t rh = ln.r_head.load(std::memory_order_acquire);
     for (;;) {
+      // the bytes of a packet a few ahead: a forwarder's source is usually a completion in another queue's
+      // ring, written by the GPU and so not in this core's caches; its first lines' misses overlap this copy
+      if (k + q->prefetch < n && q->prefetch) {
+        const uint8_t* a = p[k + q->prefetch].data;
+        const uint32_t nb = p[k + q->prefetch].len + (mode == WG_MODE_OPEN ? 16u : 0u);
+        for (uint32_t o = 0; o < nb; o += 64u) __builtin_prefetch(a + o, 0, 0);
+      }
       queue_fill(q, s, p[k].key_slot, p[k].counter, p[k].data, p[k].len, p[k].user);
       ln.ready[rt % q->per_lane] = s;
       ++rt;
@@ -615,6 +623,7 @@ int wg_queue_create(wg_ctx* c, int mode, uint32_t capacity, uint32_t max_len, ui
   if (const char* e = getenv("WG_QUEUE_MIN_BATCH")) q->min_batch = (uint32_t)std::max(1, atoi(e));
   if (const char* e = getenv("WG_QUEUE_WINDOW_US")) q->window_ns = 1000ull * (uint64_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_QUEUE_STEAL")) q->steal = atoi(e) != 0;
+  if (const char* e = getenv("WG_QUEUE_PREFETCH")) q->prefetch = (uint32_t)std::max(0, std::min(8, atoi(e)));
   q->min_batch = std::min(q->min_batch, q->max_batch);
   q->wake_batch = std::max(1u, std::min(256u, q->cap / 8u));
   q->meta.reset(new wgq::SlotMeta[q->cap]());
