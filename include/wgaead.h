@@ -372,7 +372,9 @@ int wg_open_host(wg_ctx* ctx, const wg_pkt* desc_host, uint32_t n, const uint8_t
  *     order from one thread, but with one lane lock and one publication per run of free slots.
  *     Returns how many were queued: n, or fewer (at least 1) when the submit timeout ran out
  *     partway; WG_EAGAIN when it ran out before the first. Every entry is checked first: a bad one
- *     fails the call (WG_EINVAL / WG_E2BIG / WG_ERANGE) with nothing queued.
+ *     fails the call (WG_EINVAL / WG_E2BIG / WG_ERANGE) with nothing queued. While it copies packet
+ *     k it prefetches the bytes of packet k + 2 (WG_QUEUE_PREFETCH=0..8 sets the distance), so
+ *     handing over completions of another queue (GPU-written, not in this core's caches) is fast.
  *   wg_reap(q, out, max, timeout_us): up to max completions (waits up to timeout_us for the
  *     first); returns how many, or a negative error. completion.data points into the queue's
  *     pinned ring: ct || tag (len + 16 B) for a seal, the plaintext (len B, valid when status is
