@@ -132,6 +132,9 @@ static void* verifier(void* arg) {
     const uint64_t now = now_ns();
     const uint64_t j0 = atomic_fetch_add(&g_no, (uint64_t)(n > 0 ? n : 0));
     for (int k = 0; k < n; ++k) {
+      /* a consumer of GPU-written completions prefetches a few ahead (as wg_submit_*_n does) */
+      if (k + 2 < n)
+        for (uint32_t o = 0; o < c[k + 2].len; o += 64) __builtin_prefetch(c[k + 2].data + o, 0, 0);
       if (j0 + k < LAT_SAMPLES) g_lat_o[j0 + k] = (now - c[k].submit_ns) * 1e-3;
       fill(want, c[k].user, c[k].len);
       if (c[k].status != WG_PKT_OK || c[k].len != pkt_len(c[k].user) || memcmp(c[k].data, want, c[k].len) != 0)
