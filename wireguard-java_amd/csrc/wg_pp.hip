@@ -781,7 +781,8 @@ uint32_t pp_claim(PPServer* S, uint32_t start, uint64_t k) {
   for (uint32_t spin = 0;; ++spin) {
     for (uint32_t d = 0; d < wgpp::kRing; ++d) {
       const uint32_t i = (start + d) % wgpp::kRing;
-      uint32_t st = S->state[i].load(std::memory_order_relaxed);
+      // acquire: an ORPHAN entry's pub[i] (stored before the release that made it ORPHAN) is read below
+      uint32_t st = S->state[i].load(std::memory_order_acquire);
       if (st == kOrphan && (__atomic_load_n((const uint64_t*)S->done(i), __ATOMIC_ACQUIRE) >> 8) ==
                                S->pub[i].load(std::memory_order_relaxed)) {
         if (S->state[i].compare_exchange_strong(st, kBusy, std::memory_order_acquire)) return i;
