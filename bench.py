@@ -76,6 +76,12 @@ def splitmix_np(seed: int, n: int) -> np.ndarray:
     return z.astype("<u8").view(np.uint8)[:n].copy()
 
 
+def imix_lengths(seed: int, n: int) -> np.ndarray:
+    """Simple IMIX payload lengths: 40, 576 and 1500 B with probabilities 7/12, 4/12 and 1/12."""
+    u = splitmix_np(seed, 4 * n).view("<u4") % 12
+    return np.where(u < 7, 40, np.where(u < 11, 576, 1500)).astype(np.int64)
+
+
 def build_workload(name: str, rank: int, world: int, packets: int = 0, keys: int = 0):
     """Per-rank packet batch: (lengths, key_slot per packet, counters, nkeys, description).
     packets / keys (diagnostic runs only, --packets / --keys): another batch size or session count
@@ -95,6 +101,15 @@ def build_workload(name: str, rank: int, world: int, packets: int = 0, keys: int
         counters = (np.arange(n, dtype=np.uint64) // k)
         tag = "" if (n, k) == (65536, 256) else f" [diagnostic: {n} packets, {k} keys]"
         return lengths, slots, counters, k, f"C2: {n} packets per GPU, 64..9000B, 256 session keys{tag}", False
+    if name == "imix":
+        # "also report an IMIX-like mix": simple IMIX, inner packets of 40 / 576 / 1500 B
+        # in the ratio 7 : 4 : 1 (seeded draw per packet), C2's 256 sessions
+        n, k = packets or 65536, keys or 256
+        lengths = imix_lengths(seed, n)
+        slots = np.arange(n, dtype=np.int64) % k
+        counters = (np.arange(n, dtype=np.uint64) // k)
+        tag = "" if (n, k) == (65536, 256) else f" [diagnostic: {n} packets, {k} keys]"
+        return lengths, slots, counters, k, f"IMIX: {n} packets per GPU, 40/576/1500B at 7:4:1, 256 session keys{tag}", False
     if name == "c3":
         total, L, sessions = 8 * 1024 * 1024, 1420, 1024
         # session s -> GPU s mod world; each session's packets carry its own counters
@@ -335,7 +350,7 @@ def main():
     # MI355X raises its clocks over the first tens of ms of load (a 20-step run measured
     # 961-1027 GiB/s on C1, 1220 once ramped; profiles/r01_kernel_study.md §5)
     ap.add_argument("--ramp-ms", type=float, default=150.0)
-    ap.add_argument("--workload", default="c1", choices=["c1", "c2", "c3", "c4"])
+    ap.add_argument("--workload", default="c1", choices=["c1", "c2", "c3", "c4", "imix"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-mem", default="pinned", choices=["pinned", "pageable"])
     # --streams K: each step's batch as K runs of consecutive packets, each sealed and opened on its own

@@ -94,6 +94,53 @@ def test_c2_full_every_packet(engine, path):
     assert np.array_equal(b, want)
 
 
+def test_imix_every_packet(engine):
+    """bench.py --workload imix (SURVEY.md §8d's IMIX-like mix: 40 / 576 / 1500 B at 7 : 4 : 1, 256
+    sessions) through the one k_step launch its line times: every ct || tag against the oracle, every
+    plaintext back, 1% forged tags rejected with their plaintext scrubbed."""
+    import bench
+    torch, dev = _dev()
+    W = wg()
+    lengths, slots, counters, nkeys, _, uniform = bench.build_workload("imix", 0, 1)
+    assert not uniform and nkeys == 256
+    n = len(lengths)
+    S = ((lengths + 16 + 15) // 16) * 16
+    off = np.concatenate([[0], np.cumsum(S)[:-1]]).astype(np.uint64)
+    total = int(S.sum())
+    desc = W.pack_desc(off, off, counters, lengths, slots)
+    keys = splitmix_np(0xC0FFEE, 32 * nkeys)
+    pt = splitmix_np(0x5EED2028, total)
+    engine.set_keys(0, keys.tobytes())
+    d = torch.from_numpy(W.desc_as_int64(desc)).to(dev)
+    dct = torch.zeros(total, dtype=torch.uint8, device=dev)
+    back = torch.zeros(total, dtype=torch.uint8, device=dev)
+    st = torch.full((n,), 7, dtype=torch.int32, device=dev)
+    engine.duplex(d, torch.from_numpy(pt).to(dev), dct, 1500, d, dct, back, st, 1500, uniform=False, after_seal=True)
+    torch.cuda.synchronize()
+    ref = np.zeros(total, np.uint8)
+    O.seal_batch(desc, pt, ref, keys, threads=16)
+    got = dct.cpu().numpy()
+    assert np.array_equal(got, ref)
+    assert int(st.abs().sum().item()) == 0
+    want = pt.copy()
+    for i in range(n):
+        want[int(off[i]) + int(lengths[i]):int(off[i]) + int(S[i])] = 0  # slack: never written
+    assert np.array_equal(back.cpu().numpy(), want)
+    bad = np.nonzero(splitmix_np(98, n) < 3)[0]
+    for i in bad:
+        got[int(off[i]) + int(lengths[i]) + 15] ^= 0x80
+    back.zero_()
+    st.fill_(7)
+    engine.open(d, torch.from_numpy(got).to(dev), back, st, 1500)
+    torch.cuda.synchronize()
+    exp = np.zeros(n, np.int32)
+    exp[bad] = 1
+    assert np.array_equal(st.cpu().numpy(), exp)
+    for i in bad:
+        want[int(off[i]):int(off[i]) + int(lengths[i])] = 0  # unauthenticated plaintext scrubbed
+    assert np.array_equal(back.cpu().numpy(), want)
+
+
 @pytest.mark.parametrize("n", [65536, 131072, 50000])
 def test_k_step_claim_every_packet(n):
     """WG_CLAIM=1: mixed-length WG_F_AFTER_SEAL steps through k_step_claim, whose slots claim their

@@ -183,14 +183,15 @@ def test_after_seal_ragged_sizes(n, L):
         eng.close()
 
 
-@pytest.mark.parametrize("n", [3000, 40000])
-@pytest.mark.parametrize("plan", [None, "WG_SLOT16=0", "WG_SLOT16=1", "WG_MIXED_SPLIT=4"])
+@pytest.mark.parametrize("n", [3000, 30000, 40000])
+@pytest.mark.parametrize("plan", [None, "WG_SLOT16=0", "WG_SLOT16=1", "WG_MIXED_SPLIT=4", "WG_SLOT4=1", "WG_SLOT4=2"])
 def test_after_seal_mixed_lengths(n, plan, monkeypatch):
     """Mixed lengths, ordered longest-first once for both halves. plan None: the size-based plan
     (3000 packets: one per slot, 16-lane slots above one round; 40000: 16-lane longest-first
-    pairs); the others force 8-lane pairs, 16-lane pairs or a split at 4 rounds (read when the
-    context is created)."""
-    for var in ("WG_SLOT16", "WG_MIXED_SPLIT"):
+    pairs); the others force 8-lane pairs, 16-lane pairs, a split at 4 rounds, 4-lane slots or
+    the long packets in 16-lane and the rest in 4-lane slots (read when the context is created; 30000 packets in 4-lane slots are 1875 waves, so the second,
+    partial generation of 1024 waves takes its positions reversed)."""
+    for var in ("WG_SLOT16", "WG_MIXED_SPLIT", "WG_SLOT4"):
         monkeypatch.delenv(var, raising=False)
     if plan:
         k, v = plan.split("=")

@@ -404,6 +404,21 @@ def test_randomized_batches_16_lane_slots(torch_dev, it, monkeypatch):
         eng.close()
 
 
+@pytest.mark.parametrize("plan", ["1", "2"])
+@pytest.mark.parametrize("it", [1, 2, 4, 5, 7])
+def test_randomized_batches_4_lane_slots(torch_dev, it, plan, monkeypatch):
+    """The same random mixed-length batches with 4-lane slots (rounds of 4 blocks, 16 slots per wave,
+    descriptors as 8-B pairs per lane, 2-step r-power scan, 2-step slot sum). WG_SLOT4=1: every packet
+    in a 4-lane slot; 2: packets of more than two 8-block rounds in 16-lane slots, the rest in 4-lane
+    slots (k_*_mixed<4>, the size-based plan for large batches of packets up to 2048 B)."""
+    monkeypatch.setenv("WG_SLOT4", plan)
+    eng = wg().Engine(0, key_slots=4096)
+    try:
+        _randomized_batch(eng, torch_dev, it)
+    finally:
+        eng.close()
+
+
 def _randomized_batch(engine, torch_dev, it):
     rng = np.random.default_rng(1000 + it)
     n = int(rng.integers(1, 2500))

@@ -100,10 +100,16 @@ struct wg_ctx {
   uint32_t key_slots = 0;
   uint32_t* keys = nullptr;               // device key table
   const uint32_t* receivers = nullptr;    // device receiver_index per key slot (WG_F_FRAME; caller-owned)
-  // waves resident at once (occupancy) of k_transport<SEAL>, <OPEN> and k_step, with 8-lane [0] and
-  // 16-lane [1] slots
-  uint32_t resident_waves[2][3] = {{0, 0, 0}, {0, 0, 0}};
+  // waves resident at once (occupancy) of k_transport<SEAL>, <OPEN> and k_step, with 8-lane [0],
+  // 16-lane [1] and 4-lane [2] slots (rw_row)
+  uint32_t resident_waves[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
   int slot16 = -1;                        // mixed batches: -1 planned (slot_plan), 0 / 1 force 8- / 16-lane slots (WG_SLOT16)
+  // mixed batches of short packets (WG_SLOT4): -1 planned (16-lane slots for the long packets, 4-lane for the
+  // rest), 0 never, 1 always 4-lane slots for every packet, 2 always the 16 / 4 split
+  int slot4 = -1;
+  bool slot4_pairs = false;               // 4-lane slots in longest-first pairs even when one packet per slot fits (A/B)
+  bool slot4_snake = true;                // 4-lane slots: odd workgroup generations reversed (WG_SLOT4_SNAKE=0: not; A/B)
+  uint32_t cus = 0;                       // compute units
   int prio_mode = -1;                     // progress-based issue priority: -1 mixed batches only, 0 off, 1 on (WG_PRIO)
   uint32_t uniform16 = 8;                 // uniform batches of n <= S8 / k packets in 16-lane slots (WG_UNIFORM16=k; 0 never)
   uint32_t mixed_split = 0;               // > 0: mixed batches one packet per slot, packets of more than this
@@ -385,6 +391,9 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   // turn): about 4 waves per SIMD, every slot with a similar share. Measured on 131072 C2-shaped
   // packets: 4 per slot (4096 waves) 1,322 GiB/s, 2 per slot (8192 waves) 1,208, 3 per slot 1,148.
   if (!(flags & WG_F_UNIFORM) && 2ull * n > cap_slots) per_slot = 2 * ((n + cap_slots - 1) / cap_slots);
+  // 4-lane slots (16 per wave) hold a 65,536-packet batch one packet per slot at 4 waves per SIMD; pairs
+  // would halve the waves (WG_SLOT4_PAIRS=1: pairs as for 8-lane slots, A/B)
+  if (G == 4 && !c->slot4_pairs && n <= cap_slots) per_slot = 1;
 #ifndef WG_PERSISTENT_UNIFORM
   // uniform lengths: one packet per slot and as many waves as that takes; the hardware
   // dispatcher starts each new wave as an old one retires, so a wave's packet-start
@@ -397,6 +406,10 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   const uint32_t waves = (uint32_t)((n + spw * per_slot - 1) / (spw * per_slot));
   const uint32_t grid = mixed ? (n + 4u * wgt::TW - 1u) / (4u * wgt::TW) + 2u : (waves + wgt::TW - 1) / wgt::TW;
   P.slots = grid * wgt::TW * spw;
+  // 4-lane slots, one packet each, longest first: all waves are resident at once, and wave w shares its
+  // SIMD with waves w + 4 x CUs k; reversing every other generation of 4 x CUs waves deals each SIMD long
+  // and short packets in turn (without it a SIMD holding the longest packets ran alone at the end)
+  if (G == 4 && per_slot == 1 && c->slot4_snake) P.wave_gen = wgt::TW * c->cus;
   if (claim) {  // k_step_claim: the largest power of two <= claim_nc that divides the grid (every sub-order
                 // then has the same number of workgroups, and its static first positions end at claim_base)
     uint32_t nc = claim_nc;
@@ -414,7 +427,9 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   if (c->prio_mode == 0) P.prio_step = 0;  // WG_PRIO=0 / 1: issue priority off / on for every batch (A/B)
   else if (c->prio_mode == 1) P.prio_step = pstep;
   if (mixed && c->prio_mode != 1) P.prio_step = 0;
-  if (!(flags & WG_F_UNIFORM) && (per_slot > 1 || mixed)) {  // longest-first order (LPT)
+  // longest-first order (LPT); 4-lane slots always (one packet per slot: a wave then holds 16 packets of
+  // about one length instead of running as long as the longest of 16 random ones)
+  if (!(flags & WG_F_UNIFORM) && (per_slot > 1 || mixed || G == 4)) {
     // reuse_order: the order already in lpt_order (the seal of the same packets, WG_F_AFTER_SEAL);
     // private_ws: buffers owned by the caller's stream (no shared-workspace ordering)
     if (!reuse_order) {
@@ -458,16 +473,27 @@ bool open_overlaps(const uint8_t* in, uint64_t in_size, const uint8_t* out, uint
 //     slot, longest first (k_transport_mixed / k_step_mixed).
 // C2-shaped batches (64..9000 B): 16384 packets 722 -> 1152 GiB/s, 32768 909 -> 1321 against the
 // 8-lane pairs; 65536 stays on them. WG_SLOT16 / WG_MIXED_SPLIT force a plan (A/B).
+//   mixed, n >= 3/4 S8 and max_len <= kSlot4MaxLen: one packet per slot, packets of more than two 8-block
+//     rounds in 16-lane slots and the rest in 4-lane slots (k_*_mixed<4>). Short packets waste most of an
+//     8-block round (a 40-B packet is 2 blocks) and pay the per-packet work (r-power scan, finish, slot
+//     sum) once per 8 packets of a wave instead of 16; the long ones in 16 lanes keep the slowest wave
+//     short (IMIX 40 / 576 / 1500 B, bench.py --workload imix: DESIGN.md §4.1).
 struct SlotPlan {
   uint32_t G;      // lanes per slot
   uint32_t split;  // > 0: one packet per slot, packets of more than `split` 8-block rounds in 16-lane slots
+  uint32_t gs = 8;  // with a split: lanes of the other packets' slots (8 or 4)
 };
-SlotPlan slot_plan(const wg_ctx* c, uint32_t flags, uint32_t n) {
+constexpr uint32_t kSlot4MaxLen = 2048;
+inline int rw_row(uint32_t G) { return G == 16 ? 1 : G == 4 ? 2 : 0; }
+SlotPlan slot_plan(const wg_ctx* c, uint32_t flags, uint32_t n, uint32_t max_len) {
   if (flags & WG_F_UNIFORM)  // small uniform batches: twice the waves in 16-lane slots (8192 x 1420 B: 665 -> 750 GiB/s)
     return {c->uniform16 > 0 && (uint64_t)n * c->uniform16 <= 8ull * c->resident_waves[0][0] ? 16u : 8u, 0u};
-  if (c->mixed_split > 0) return {8u, c->mixed_split};
+  if (c->mixed_split > 0) return {8u, c->mixed_split, c->slot4 == 2 ? 4u : 8u};
+  if (c->slot4 == 1) return {4u, 0u};
+  if (c->slot4 == 2) return {8u, 2u, 4u};
   if (c->slot16 >= 0) return {c->slot16 ? 16u : 8u, 0u};
   const uint64_t s8 = 8ull * c->resident_waves[0][0];
+  if (4ull * n >= 3ull * s8 && c->slot4 != 0 && max_len <= kSlot4MaxLen) return {8u, 2u, 4u};
   if (4ull * n >= 3ull * s8) return {8u, 0u};
   if (8ull * n >= 3ull * s8) return {16u, 0u};
   return {8u, 1u};
@@ -528,9 +554,9 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
   wgt::TransportParams P{};
   uint32_t grid = 0;
   bool ordered = false;
-  const SlotPlan sp = slot_plan(c, flags, n);
+  const SlotPlan sp = slot_plan(c, flags, n, max_len);
   const uint32_t G = sp.G;
-  const uint64_t cap_waves = std::max<uint32_t>(c->resident_waves[G == 16][MODE == WG_MODE_OPEN], wgt::TW);
+  const uint64_t cap_waves = std::max<uint32_t>(c->resident_waves[rw_row(G)][MODE == WG_MODE_OPEN], wgt::TW);
   const bool own = own_hist && own_order;  // the caller holds the plan workspace (launch_after_seal)
   int rc = plan_transport<MODE>(c, desc, n, in, in_size, out, out_size, status, max_len, flags, s, cap_waves, G,
                                 own ? *own_hist : c->lpt_hist, own ? *own_order : c->lpt_order, &P, &grid, &ordered,
@@ -545,8 +571,11 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
   if (!own_keys) record_start(c, s, &ev);
   if constexpr (MODE == WG_MODE_OPEN) {
     if (open_overlaps(in, in_size, out, out_size)) {  // in-place opens verify first (k_transport<OPEN, G, true>)
-      if (P.n_long) hipLaunchKernelGGL((wgt::k_transport_mixed<MODE, true>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
+      if (P.n_long && sp.gs == 4)
+        hipLaunchKernelGGL((wgt::k_transport_mixed<MODE, true, 4>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
+      else if (P.n_long) hipLaunchKernelGGL((wgt::k_transport_mixed<MODE, true>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
       else if (G == 16) hipLaunchKernelGGL((wgt::k_transport<MODE, 16, true>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
+      else if (G == 4) hipLaunchKernelGGL((wgt::k_transport<MODE, 4, true>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
       else hipLaunchKernelGGL((wgt::k_transport<MODE, 8, true>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
       const hipError_t e = hipGetLastError();
       record_end(c, s, ev);
@@ -554,8 +583,11 @@ int launch_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* i
       return ordered ? ws_release(c, s) : WG_OK;
     }
   }
-  if (P.n_long) hipLaunchKernelGGL((wgt::k_transport_mixed<MODE>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
+  if (P.n_long && sp.gs == 4)
+    hipLaunchKernelGGL((wgt::k_transport_mixed<MODE, false, 4>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
+  else if (P.n_long) hipLaunchKernelGGL((wgt::k_transport_mixed<MODE>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
   else if (G == 16) hipLaunchKernelGGL((wgt::k_transport<MODE, 16>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
+  else if (G == 4) hipLaunchKernelGGL((wgt::k_transport<MODE, 4>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
   else hipLaunchKernelGGL((wgt::k_transport<MODE, 8>), dim3(grid), dim3(64 * wgt::TW), 0, s, P);
   const hipError_t e = hipGetLastError();
   record_end(c, s, ev);
@@ -572,7 +604,8 @@ hipStream_t pick_stream(wg_ctx*, void* stream) { return (hipStream_t)stream; }
 int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStream_t s) {
   const bool same_plan = sb->max_len == ob->max_len && (sb->flags & WG_F_UNIFORM) == (ob->flags & WG_F_UNIFORM) &&
                          c->resident_waves[0][0] == c->resident_waves[0][1] &&
-                         c->resident_waves[1][0] == c->resident_waves[1][1];
+                         c->resident_waves[1][0] == c->resident_waves[1][1] &&
+                         c->resident_waves[2][0] == c->resident_waves[2][1];
   // a uniform batch is not ordered (one packet per slot): no workspace, and no event record
   // between one step's open and the next step's seal
   const bool ordered = !(sb->flags & WG_F_UNIFORM) || !(ob->flags & WG_F_UNIFORM);
@@ -592,9 +625,9 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
   int rc;
   if (ordered && (rc = ws_acquire(c, s)) != WG_OK) return rc;
   if (fused) {
-    const SlotPlan sp = slot_plan(c, sb->flags, sb->n);
+    const SlotPlan sp = slot_plan(c, sb->flags, sb->n, sb->max_len);
     const uint32_t G = sp.G;
-    const uint64_t cap = std::max<uint32_t>(c->resident_waves[G == 16][2], wgt::TW);
+    const uint64_t cap = std::max<uint32_t>(c->resident_waves[rw_row(G)][2], wgt::TW);
     wgt::TransportParams PS{}, PO{};
     uint32_t gs = 0, go = 0;
     bool os = false, oo = false;
@@ -629,10 +662,12 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
       hipEvent_t ev;
       record_start(c, s, &ev);
       if (claim_nc) hipLaunchKernelGGL((wgt::k_step_claim<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
-      else if (PS.n_long) hipLaunchKernelGGL(wgt::k_step_mixed, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+      else if (PS.n_long && sp.gs == 4) hipLaunchKernelGGL(wgt::k_step_mixed<4>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+      else if (PS.n_long) hipLaunchKernelGGL(wgt::k_step_mixed<8>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else if (c->test_flip && G == 8)  // test hook build: the same body with the tag flip between the halves
         hipLaunchKernelGGL((wgt::k_step<8, 4, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, c->test_flip);
       else if (G == 16) hipLaunchKernelGGL(wgt::k_step<16>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
+      else if (G == 4) hipLaunchKernelGGL(wgt::k_step<4>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
       else if (c->step_wpe4 && 2ull * gs * wgt::TW <= cap)
         hipLaunchKernelGGL((wgt::k_step<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
       else hipLaunchKernelGGL(wgt::k_step<8>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
@@ -697,7 +732,7 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   c->key_slots = key_slots;
   c->ws_stream = (hipStream_t)-1;
   hipDeviceProp_t prop;
-  int bl[2][3] = {{0, 0, 0}, {0, 0, 0}};  // workgroups per CU of each transport kernel
+  int bl[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};  // workgroups per CU of each transport kernel
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->copy_out_stream, hipStreamNonBlocking) != hipSuccess ||
@@ -716,6 +751,11 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&bl[1][1], wgt::k_transport<WG_MODE_OPEN, 16>, 64 * wgt::TW, 0) !=
           hipSuccess ||
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&bl[1][2], wgt::k_step<16>, 64 * wgt::TW, 0) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&bl[2][0], wgt::k_transport<WG_MODE_SEAL, 4>, 64 * wgt::TW, 0) !=
+          hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&bl[2][1], wgt::k_transport<WG_MODE_OPEN, 4>, 64 * wgt::TW, 0) !=
+          hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&bl[2][2], wgt::k_step<4>, 64 * wgt::TW, 0) != hipSuccess ||
       hipMalloc(&c->keys, (size_t)key_slots * 32) != hipSuccess ||
       // on the context's stream, like every later key write: a memset on the null stream can sit
       // behind another context's per-packet server in a shared hardware queue and land AFTER the
@@ -727,15 +767,20 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   }
   c->key_words.reset(new std::atomic<uint64_t>[(size_t)key_slots * 4]());
   c->key_seq.reset(new std::atomic<uint32_t>[key_slots]());
-  for (int w = 0; w < 2; ++w)
+  c->cus = (uint32_t)prop.multiProcessorCount;
+  for (int w = 0; w < 3; ++w)
     for (int k = 0; k < 3; ++k)
       c->resident_waves[w][k] = (uint32_t)std::max(bl[w][k], 1) * wgt::TW * (uint32_t)prop.multiProcessorCount;
   // Scheduling overrides for A/B measurements (tools/ab_args.sh), read once per context; none
   // changes a byte of output (the parity suite runs each): WG_SLOT16=0|1 (mixed batches in 8- or
-  // 16-lane slots), WG_MIXED_SPLIT=R (mixed batches one packet per slot, packets of more than R
+  // 16-lane slots), WG_SLOT4=0|1|2 (mixed batches never / always in 4-lane slots /
+  // always long ones in 16-lane and the rest in 4-lane slots), WG_MIXED_SPLIT=R (mixed batches one packet per slot, packets of more than R
   // 8-block rounds in 16-lane slots), WG_UNIFORM16=k (uniform batches of at most S8/k packets in
   // 16-lane slots, 0 never), WG_PRIO=0|1 (issue-priority schedule off / on for every batch).
   if (const char* e = getenv("WG_SLOT16")) c->slot16 = atoi(e);
+  if (const char* e = getenv("WG_SLOT4")) c->slot4 = atoi(e);
+  if (const char* e = getenv("WG_SLOT4_PAIRS")) c->slot4_pairs = atoi(e) != 0;
+  if (const char* e = getenv("WG_SLOT4_SNAKE")) c->slot4_snake = atoi(e) != 0;
   if (const char* e = getenv("WG_MIXED_SPLIT")) c->mixed_split = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_UNIFORM16")) c->uniform16 = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_PRIO")) c->prio_mode = atoi(e);

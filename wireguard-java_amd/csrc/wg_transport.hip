@@ -132,6 +132,10 @@ struct TransportParams {
   uint32_t claim_base;    // slots per sub-order = the counters' initial value
   uint2* chain_out;       // seal half of k_step_claim: per position {next position, next packet} of its slot
   const uint2* chain_in;  // open half: the same chain, replayed (slot g opens exactly what it sealed)
+  // 4-lane slots, one packet per slot (plan_transport): waves in one workgroup generation (workgroups
+  // per CU x CUs x waves per workgroup); every odd generation takes its longest-first positions in
+  // reverse, so the waves that share a SIMD get long and short packets in turn (0: no reversal)
+  uint32_t wave_gen;
 #ifdef WG_DIAG
   uint64_t* stamps;       // diagnostic build only: 10 x u64 per wave (cycles per phase, start/end times)
 #endif
@@ -162,11 +166,11 @@ struct TransportParams {
 #define WG_PH_STORE(idx) do {} while (0)
 #endif
 
-// ---- lane exchange inside a slot of G lanes (G = 8 or 16) ---------------------------
+// ---- lane exchange inside a slot of G lanes (G = 4, 8 or 16) ------------------------
 // ds_swizzle bitmask mode inside each 32-lane half: src = ((lane & and) | or) ^ xor.
 template <int G, int K>
 __device__ __forceinline__ uint32_t bcastg(uint32_t v) {  // every lane of the slot reads lane K of it
-  static_assert(G == 8 || G == 16, "slots of 8 or 16 lanes");
+  static_assert(G == 4 || G == 8 || G == 16, "slots of 4, 8 or 16 lanes");
   return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (0x20 - G) | (K << 5));
 }
 template <int K>
@@ -174,6 +178,18 @@ __device__ __forceinline__ uint32_t bcast8(uint32_t v) { return bcastg<8, K>(v);
 template <int X>
 __device__ __forceinline__ uint32_t xorg(uint32_t v) {  // lane reads lane ^ X (X < 16)
   return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1f | (X << 10));
+}
+
+// A slot's copy of one 32-B descriptor (wg_pkt = 8 dwords): with 8 or 16 lanes, lane j holds dword j & 7
+// (w0); with 4 lanes, lane j holds dwords 2j and 2j + 1 (w0, w1: one 8-B load, desc_load4). desc_word<G, K>
+// gives every lane of the slot dword K.
+__device__ __forceinline__ uint2 desc_load4(const wg_pkt* d, uint32_t i, uint32_t j) {
+  return i != ~0u ? ((const uint2*)(d + i))[j & 3u] : make_uint2(0u, 0u);
+}
+template <int G, int K>
+__device__ __forceinline__ uint32_t desc_word(uint32_t w0, uint32_t w1) {
+  if constexpr (G == 4) return bcastg<4, K / 2>((K & 1) ? w1 : w0);
+  else return bcastg<G, K>(w0);
 }
 
 // The same exchanges through DPP (VALU, no LDS round trip) for the dependent chains of the
@@ -328,15 +344,23 @@ template <int MODE, int G = 8, bool VF = false, int PM = kPosStatic>
 __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_t blk, uint32_t wv, uint4* const img,
                                                SlotRec* const rec, uint32_t& iter) {
   static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
-  static_assert(G == 8 || G == 16, "slots of 8 or 16 lanes");
+  static_assert(G == 4 || G == 8 || G == 16, "slots of 4, 8 or 16 lanes");
   static_assert(!VF || MODE == WG_MODE_OPEN, "verify-first is an open variant");
-  constexpr uint32_t SH = G == 8 ? 3u : 4u;  // log2 G
+  constexpr uint32_t SH = G == 4 ? 2u : G == 8 ? 3u : 4u;  // log2 G
   constexpr uint32_t JM = G - 1u;
   if (P.prio_step && iter == 0) __builtin_amdgcn_s_setprio(3);  // first instruction: a fresh wave is never starved
   const uint32_t S = P.slots;
-  const uint32_t g = (blk * TW + wv) * (64u / G) + (opaque_lane() >> SH);
+  uint32_t wg = blk * TW + wv;  // this wave's index in the grid
+  if constexpr (G == 4) {
+    if (P.wave_gen) {  // odd generations reversed (a bijection: the last, partial one over its own size)
+      const uint32_t k = wg / P.wave_gen, i = wg - k * P.wave_gen;
+      const uint32_t size = min(P.wave_gen, gridDim.x * TW - k * P.wave_gen);
+      if (k & 1u) wg = k * P.wave_gen + (size - 1u - i);
+    }
+  }
+  const uint32_t g = wg * (64u / G) + (opaque_lane() >> SH);
 
-  // descriptor prefetch: dword j of the next packet's wg_pkt (32 B = 8 dwords, one per lane)
+  // descriptor prefetch: the next packet's wg_pkt spread over the slot's lanes (desc_load)
   uint32_t gen = 0;
   uint32_t nxt;
   // kPosClaim / kPosChain: the sub-order of this workgroup and the positions of the next / current packet
@@ -353,7 +377,14 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
     npos = pos;
     nxt = pos < P.n ? (P.order ? P.order[pos] : pos) : ~0u;
   }
-  uint32_t dnext = nxt != ~0u ? ((const uint32_t*)(P.desc + nxt))[opaque_lane() & 7u] : 0u;
+  uint32_t dnext = 0u, dnext2 = 0u;
+  if constexpr (G == 4) {
+    const uint2 w = desc_load4(P.desc, nxt, opaque_lane());
+    dnext = w.x;
+    dnext2 = w.y;
+  } else {
+    dnext = nxt != ~0u ? ((const uint32_t*)(P.desc + nxt))[opaque_lane() & 7u] : 0u;
+  }
 
   bool have = false;
   uint32_t pkt = 0, round = 0;
@@ -385,12 +416,12 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
       const uint32_t lane = opaque_lane(), s = lane >> SH, j = lane & JM;
       pkt = nxt;
 #ifdef WG_DIAG
-      { uint32_t dn = dnext; asm volatile("s_waitcnt vmcnt(0)" : "+v"(dn)); dnext = dn; }
+      { uint32_t dn = dnext, dn2 = dnext2; asm volatile("s_waitcnt vmcnt(0)" : "+v"(dn), "+v"(dn2)); dnext = dn; dnext2 = dn2; }
       WG_PH(6);
 #endif
-      const uint32_t d0 = bcastg<G, 0>(dnext), d1 = bcastg<G, 1>(dnext), d2 = bcastg<G, 2>(dnext),
-                     d3 = bcastg<G, 3>(dnext);
-      const uint32_t len = bcastg<G, 6>(dnext), ks = bcastg<G, 7>(dnext);
+      const uint32_t d0 = desc_word<G, 0>(dnext, dnext2), d1 = desc_word<G, 1>(dnext, dnext2),
+                     d2 = desc_word<G, 2>(dnext, dnext2), d3 = desc_word<G, 3>(dnext, dnext2);
+      const uint32_t len = desc_word<G, 6>(dnext, dnext2), ks = desc_word<G, 7>(dnext, dnext2);
       const uint64_t in_off = (uint64_t)d0 | ((uint64_t)d1 << 32);
       const uint64_t out_off = (uint64_t)d2 | ((uint64_t)d3 << 32);
       const bool valid =
@@ -419,11 +450,25 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         uint32_t v = k[0];
 #pragma unroll
         for (uint32_t i = 1; i < 8u; ++i) v = j == i ? k[i] : v;
-        if (valid && j < 8u) ((uint32_t*)rec[s].key)[j] = v;
+        if constexpr (G == 4) {  // 4 lanes: key words j and j + 4
+          uint32_t v2 = k[4];
+#pragma unroll
+          for (uint32_t i = 1; i < 4u; ++i) v2 = j == i ? k[4u + i] : v2;
+          if (valid) {
+            ((uint32_t*)rec[s].key)[j] = v;
+            ((uint32_t*)rec[s].key)[j + 4u] = v2;
+          }
+        } else if (valid && j < 8u) {
+          ((uint32_t*)rec[s].key)[j] = v;
+        }
+      } else if (valid && G == 4) {
+        ((uint32_t*)rec[s].key)[j] = P.keys[8u * ks + j];
+        ((uint32_t*)rec[s].key)[j + 4u] = P.keys[8u * ks + j + 4u];
       } else if (valid && j < 8u) {
         ((uint32_t*)rec[s].key)[j] = P.keys[8u * ks + j];
       }
-      const uint32_t c0 = bcastg<G, 4>(dnext), c1 = bcastg<G, 5>(dnext);  // all lanes active: swizzles read live lanes
+      // all lanes active: swizzles read live lanes
+      const uint32_t c0 = desc_word<G, 4>(dnext, dnext2), c1 = desc_word<G, 5>(dnext, dnext2);
       if (j == 0) {
         rec[s].addr = make_uint4(d0, d1, d2, d3);
         rec[s].meta = make_uint4(c0, c1, len, (valid ? 1u : 0u) | al);
@@ -449,7 +494,13 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         npos = cn.x;
         nxt = cn.y;
       }
-      dnext = nxt != ~0u ? ((const uint32_t*)(P.desc + nxt))[j & 7u] : 0u;
+      if constexpr (G == 4) {
+        const uint2 w = desc_load4(P.desc, nxt, j);
+        dnext = w.x;
+        dnext2 = w.y;
+      } else {
+        dnext = nxt != ~0u ? ((const uint32_t*)(P.desc + nxt))[j & 7u] : 0u;
+      }
     }
     if (!__any(have)) break;
     wave_lds_sync();  // the slot records before the lanes read them
@@ -705,7 +756,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
           for (int i = 0; i < 5; ++i) {  // slot sum (every lane of the slot ends with it)
             acc[i] += xor1_dpp(acc[i]);
             acc[i] += xor2_dpp(acc[i]);
-            acc[i] += xor4_dpp(acc[i]);
+            if constexpr (G >= 8) acc[i] += xor4_dpp(acc[i]);
             if constexpr (G == 16) acc[i] += xor8_dpp(acc[i]);
           }
         }
@@ -772,20 +823,23 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
 // that overlap themselves verify first (kVerifyFirst); every other launch takes the one-pass body
 template <int MODE, int G = 8, bool VF = false>
 __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8))) k_transport(TransportParams P) {
-  __shared__ uint4 img_[TW][4 * 64];  // 4 KB per wave: [chunk q][lane] = the round's payload / MAC input
-  __shared__ SlotRec rec_[TW][8];     // 1 KB per wave
+  __shared__ uint4 img_[TW][4 * 64];         // 4 KB per wave: [chunk q][lane] = the round's payload / MAC input
+  __shared__ SlotRec rec_[TW][64 / G < 8 ? 8 : 64 / G];  // one record per slot: 1 KB per wave (2 KB with 4-lane slots)
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t iter = 0;
   transport_body<MODE, G, VF>(P, blockIdx.x, wv, img_[wv], rec_[wv], iter);
 }
 
-// ---- mixed-length batches: 16-lane slots for the long packets, 8-lane slots for the rest ----
+// ---- mixed-length batches: 16-lane slots for the long packets, 8- (or 4-) lane slots for the rest ----
 // The batch is ordered longest-first (k_lpt_*); the n_long packets at its front (more than
 // `split` rounds of 8 blocks) take 16-lane slots, so no slot runs much more than `split` rounds.
+// GS: lanes of the short packets' slots (8, or 4 for batches of short packets: half the ChaCha20 lanes
+// a 40-B packet leaves idle, and the per-packet work shared by 16 packets of a wave instead of 8).
 // Every slot holds ONE packet and the grid has as many workgroups as that takes (more than are
 // resident): the hardware dispatcher starts each new workgroup as an old one retires, longest
 // packets first. Workgroups [0, b16) run the 16-lane body, [b16, b16 + b8) the 8-lane body; the
 // rest of the (host-sized, upper-bound) grid exits at once.
+template <int GS = 8>
 __device__ __forceinline__ int mixed_part(const TransportParams& P, uint32_t blk, TransportParams& Q, uint32_t& qblk) {
   const uint32_t nl = min(__builtin_amdgcn_readfirstlane(*(const WG_CONST uint32_t*)P.n_long), P.n);
   const uint32_t b16 = (nl + 4u * TW - 1u) / (4u * TW);
@@ -796,44 +850,46 @@ __device__ __forceinline__ int mixed_part(const TransportParams& P, uint32_t blk
     qblk = blk;
     return 16;
   }
-  const uint32_t ns = P.n - nl, b8 = (ns + 8u * TW - 1u) / (8u * TW);
-  if (blk - b16 >= b8) return 0;
+  constexpr uint32_t spw = 64u / GS;  // short slots per wave
+  const uint32_t ns = P.n - nl, bs = (ns + spw * TW - 1u) / (spw * TW);
+  if (blk - b16 >= bs) return 0;
   Q.order = P.order + nl;
   Q.n = ns;
-  Q.slots = b8 * TW * 8u;
+  Q.slots = bs * TW * spw;
   qblk = blk - b16;
-  return 8;
+  return GS;
 }
 
-template <int MODE, bool VF = false>
+template <int MODE, bool VF = false, int GS = 8>
 __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8))) k_transport_mixed(TransportParams P) {
   __shared__ uint4 img_[TW][4 * 64];
-  __shared__ SlotRec rec_[TW][8];
+  __shared__ SlotRec rec_[TW][64 / GS];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   TransportParams Q;
   uint32_t qb = 0, iter = 0;
-  const int g = mixed_part(P, blockIdx.x, Q, qb);
+  const int g = mixed_part<GS>(P, blockIdx.x, Q, qb);
   if (g == 16) transport_body<MODE, 16, VF>(Q, qb, wv, img_[wv], rec_[wv], iter);
-  else if (g == 8) transport_body<MODE, 8, VF>(Q, qb, wv, img_[wv], rec_[wv], iter);
+  else if (g == GS) transport_body<MODE, GS, VF>(Q, qb, wv, img_[wv], rec_[wv], iter);
 }
 
+template <int GS = 8>
 __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)))
 k_step_mixed(TransportParams S, TransportParams O) {
   __shared__ uint4 img_[TW][4 * 64];
-  __shared__ SlotRec rec_[TW][8];
+  __shared__ SlotRec rec_[TW][64 / GS];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   TransportParams QS, QO;
   uint32_t qb = 0, qb2 = 0, iter = 0;
-  const int g = mixed_part(S, blockIdx.x, QS, qb);
-  (void)mixed_part(O, blockIdx.x, QO, qb2);  // the same split: the open batch has the seal's lengths
+  const int g = mixed_part<GS>(S, blockIdx.x, QS, qb);
+  (void)mixed_part<GS>(O, blockIdx.x, QO, qb2);  // the same split: the open batch has the seal's lengths
   if (g == 16) {
     transport_body<WG_MODE_SEAL, 16>(QS, qb, wv, img_[wv], rec_[wv], iter);
     asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
     transport_body<WG_MODE_OPEN, 16>(QO, qb, wv, img_[wv], rec_[wv], iter);
-  } else if (g == 8) {
-    transport_body<WG_MODE_SEAL, 8>(QS, qb, wv, img_[wv], rec_[wv], iter);
+  } else if (g == GS) {
+    transport_body<WG_MODE_SEAL, GS>(QS, qb, wv, img_[wv], rec_[wv], iter);
     asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
-    transport_body<WG_MODE_OPEN, 8>(QO, qb, wv, img_[wv], rec_[wv], iter);
+    transport_body<WG_MODE_OPEN, GS>(QO, qb, wv, img_[wv], rec_[wv], iter);
   }
 }
 
@@ -897,7 +953,7 @@ template <int G = 8, int WPE = 8, bool FLIP = false>
 __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_step(TransportParams S, TransportParams O, uint32_t test_flip) {
   __shared__ uint4 img_[TW][4 * 64];
-  __shared__ SlotRec rec_[TW][8];
+  __shared__ SlotRec rec_[TW][64 / G < 8 ? 8 : 64 / G];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t iter = 0;  // one issue-priority schedule over both halves (plan_transport: prio_step of the step)
   transport_body<WG_MODE_SEAL, G>(S, blockIdx.x, wv, img_[wv], rec_[wv], iter);
