@@ -94,14 +94,16 @@ def test_c2_full_every_packet(engine, path):
     assert np.array_equal(b, want)
 
 
-def test_imix_every_packet(engine):
+@pytest.mark.parametrize("packets", [65536, 32768, 131072])
+def test_imix_every_packet(engine, packets):
     """bench.py --workload imix (SURVEY.md §8d's IMIX-like mix: 40 / 576 / 1500 B at 7 : 4 : 1, 256
-    sessions) through the one k_step launch its line times: every ct || tag against the oracle, every
-    plaintext back, 1% forged tags rejected with their plaintext scrubbed."""
+    sessions) through the one k_step launch its line times (65,536 packets; 32,768 and 131,072 take the
+    same plan, long packets in 16-lane and the rest in 4-lane slots): every ct || tag against the
+    oracle, every plaintext back, 1% forged tags rejected with their plaintext scrubbed."""
     import bench
     torch, dev = _dev()
     W = wg()
-    lengths, slots, counters, nkeys, _, uniform = bench.build_workload("imix", 0, 1)
+    lengths, slots, counters, nkeys, _, uniform = bench.build_workload("imix", 0, 1, packets)
     assert not uniform and nkeys == 256
     n = len(lengths)
     S = ((lengths + 16 + 15) // 16) * 16

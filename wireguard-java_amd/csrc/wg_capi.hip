@@ -473,11 +473,12 @@ bool open_overlaps(const uint8_t* in, uint64_t in_size, const uint8_t* out, uint
 //     slot, longest first (k_transport_mixed / k_step_mixed).
 // C2-shaped batches (64..9000 B): 16384 packets 722 -> 1152 GiB/s, 32768 909 -> 1321 against the
 // 8-lane pairs; 65536 stays on them. WG_SLOT16 / WG_MIXED_SPLIT force a plan (A/B).
-//   mixed, n >= 3/4 S8 and max_len <= kSlot4MaxLen: one packet per slot, packets of more than two 8-block
+//   mixed, n >= 3/8 S8 and max_len <= kSlot4MaxLen: one packet per slot, packets of more than two 8-block
 //     rounds in 16-lane slots and the rest in 4-lane slots (k_*_mixed<4>). Short packets waste most of an
 //     8-block round (a 40-B packet is 2 blocks) and pay the per-packet work (r-power scan, finish, slot
 //     sum) once per 8 packets of a wave instead of 16; the long ones in 16 lanes keep the slowest wave
-//     short (IMIX 40 / 576 / 1500 B, bench.py --workload imix: DESIGN.md §4.1).
+//     short (IMIX 40 / 576 / 1500 B, bench.py --workload imix: 32,768 packets 340 -> 428 GiB/s, 65,536
+//     517 -> 660, 131,072 607 -> 820; at 16,384 and below the other plans stay 10-13% ahead: DESIGN.md §4.1).
 struct SlotPlan {
   uint32_t G;      // lanes per slot
   uint32_t split;  // > 0: one packet per slot, packets of more than `split` 8-block rounds in 16-lane slots
@@ -493,7 +494,7 @@ SlotPlan slot_plan(const wg_ctx* c, uint32_t flags, uint32_t n, uint32_t max_len
   if (c->slot4 == 2) return {8u, 2u, 4u};
   if (c->slot16 >= 0) return {c->slot16 ? 16u : 8u, 0u};
   const uint64_t s8 = 8ull * c->resident_waves[0][0];
-  if (4ull * n >= 3ull * s8 && c->slot4 != 0 && max_len <= kSlot4MaxLen) return {8u, 2u, 4u};
+  if (8ull * n >= 3ull * s8 && c->slot4 != 0 && max_len <= kSlot4MaxLen) return {8u, 2u, 4u};
   if (4ull * n >= 3ull * s8) return {8u, 0u};
   if (8ull * n >= 3ull * s8) return {16u, 0u};
   return {8u, 1u};
