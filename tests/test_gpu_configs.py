@@ -279,9 +279,10 @@ def test_k_step_mixed_c2_shape_default_plan():
         eng.close()
 
 
+@pytest.mark.parametrize("n", [40, 32768])
 @pytest.mark.parametrize("shift", [0, -8, -1])
 @pytest.mark.parametrize("uniform", [True, False])
-def test_in_place_open_keeps_forged_packets(engine, shift, uniform):
+def test_in_place_open_keeps_forged_packets(engine, shift, uniform, n):
     """Batch open whose plaintext range overlaps the ciphertext || tag range (in place, shift 0,
     or moved back by a few bytes, which a byte-sequential decrypt also allows; a forward move is
     undefined, as for the reference's sequential cipher): every such packet is verified before
@@ -289,12 +290,13 @@ def test_in_place_open_keeps_forged_packets(engine, shift, uniform):
     (verify-first: the tag pass, then a decrypt pass), as ChaCha20Poly1305.java:40-56 verifies
     before it decrypts. A good packet decrypts in place; a forged one comes back WG_PKT_BADTAG
     with its ciphertext || tag untouched. Mixed lengths (uniform False) include 0-byte and
-    multi-round packets."""
+    multi-round packets. 32,768 mixed packets of at most 2,000 B take the verify-first body of the
+    16 / 4-lane split (k_transport_mixed<OPEN, true, 4>)."""
     torch, dev = _dev()
     W = wg()
     rng = np.random.default_rng(70 + shift)
-    n = 40
-    lengths = np.full(n, 300, np.int64) if uniform else rng.integers(0, 3000, n).astype(np.int64)
+    top = 3000 if n == 40 else 2000
+    lengths = np.full(n, 300, np.int64) if uniform else rng.integers(0, top, n).astype(np.int64)
     lengths[3] = 0 if not uniform else lengths[3]
     S = ((lengths + 16 + 15) // 16) * 16 + 32
     off = (np.concatenate([[0], np.cumsum(S)[:-1]]) + 16).astype(np.uint64)
@@ -303,7 +305,7 @@ def test_in_place_open_keeps_forged_packets(engine, shift, uniform):
     pt = splitmix_np(62 + shift, total)
     sd = W.pack_desc(off, off, np.arange(n, dtype=np.uint64), lengths, np.zeros(n, np.int64))
     sealed = pt.copy()
-    O.seal_batch(sd, pt, sealed, keys, threads=1)
+    O.seal_batch(sd, pt, sealed, keys, threads=8)
     forged = rng.random(n) < 0.3
     forged[0], forged[1] = True, False
     for i in np.nonzero(forged)[0]:
