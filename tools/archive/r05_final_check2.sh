@@ -1,5 +1,5 @@
 set -o pipefail
-O=$GRAFT_REPO_ROOT/gpurun_out/r05u
+O=$GRAFT_REPO_ROOT/gpurun_out/r05v
 mkdir -p $O
 timeout -k 10 700 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "tests FAILED"; tail -40 $O/gpu_tests.log; exit 1; }
 tail -1 $O/gpu_tests.log
