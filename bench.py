@@ -121,6 +121,38 @@ def build_workload(name: str, rank: int, world: int, packets: int = 0, keys: int
     raise SystemExit(f"unknown workload {name}")
 
 
+def host_cpus(cgroup_root: str = "/sys/fs/cgroup"):
+    """CPUs this process can keep busy, and where the number comes from: the affinity mask, capped by
+    a cgroup CPU quota (v2 `cpu.max` "quota period", or v1 `cpu/cpu.cfs_quota_us` / `cfs_period_us`).
+    The same rule as the library's host_cpus() (wg_pp.hip). A GPU box here allows 16 CPUs of time while
+    its affinity covers every CPU of the machine, so os.cpu_count() alone overstates what a timing can use.
+    Returns (cpus, source) with source "quota" when the quota is the binding limit, else "affinity"."""
+    try:
+        n = len(os.sched_getaffinity(0))
+        src = "affinity"
+    except (AttributeError, OSError):
+        n, src = os.cpu_count() or 1, "cpu_count"
+    quota = None
+    try:
+        with open(os.path.join(cgroup_root, "cpu.max")) as f:
+            q, period = f.read().split()[:2]
+        if q != "max" and int(period) > 0:
+            quota = max(1, int(q) // int(period))
+    except (OSError, ValueError):
+        try:
+            with open(os.path.join(cgroup_root, "cpu", "cpu.cfs_quota_us")) as f:
+                q = int(f.read().strip())
+            with open(os.path.join(cgroup_root, "cpu", "cpu.cfs_period_us")) as f:
+                period = int(f.read().strip())
+            if q > 0 and period > 0:
+                quota = max(1, q // period)
+        except (OSError, ValueError):
+            pass
+    if quota is not None and quota < n:
+        return quota, "quota"
+    return max(1, n), src
+
+
 def oracle_sample_check(sample, keys):
     """The checker, after the timed region: the ciphertext || tag the timed kernel wrote for a seeded
     sample of packets, compared byte for byte with the CPU restatement sealing the same plaintext
@@ -128,7 +160,7 @@ def oracle_sample_check(sample, keys):
     from oracle import oracle as O
     desc, pt, ct = sample
     ref = np.zeros_like(ct)
-    O.seal_batch(desc, pt, ref, keys, threads=max(1, min(16, os.cpu_count() or 1)))
+    O.seal_batch(desc, pt, ref, keys, threads=host_cpus()[0])
     L = desc["len"].astype(np.int64)
     ok = all(np.array_equal(ct[int(o):int(o) + int(l) + 16], ref[int(o):int(o) + int(l) + 16])
              for o, l in zip(desc["in_off"], L))
@@ -136,10 +168,11 @@ def oracle_sample_check(sample, keys):
             "what": "ct||tag of a seeded sample of the timed batch vs oracle/liboracle.so sealing its plaintext"}
 
 
-def cpu_baseline(lengths, slots, counters, keys, budget_s: float = 1.5):
-    """Time the CPU restatement (oracle) on a bounded sample of the same workload."""
+def cpu_baseline(lengths, slots, counters, keys, budget_s: float = 1.5, cgroup_root: str = "/sys/fs/cgroup"):
+    """Time the CPU restatement (oracle) on a bounded sample of the same workload, on as many threads as
+    the process may keep busy (host_cpus: affinity capped by the cgroup quota), and on one thread."""
     from oracle import oracle as O
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, cores_source = host_cpus(cgroup_root)
     n = min(len(lengths), 16384)
     L = lengths[:n]
     S = ((L + 16 + 15) // 16) * 16
@@ -169,7 +202,8 @@ def cpu_baseline(lengths, slots, counters, keys, budget_s: float = 1.5):
 
     multi, m_seal, m_open, reps = run(threads, budget_s)
     single, s_seal, s_open, _ = run(1, budget_s / 3)
-    return {"value": round(multi, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+    return {"value": round(multi, 3), "unit": "GiB/s", "cores": threads, "cores_source": cores_source,
+            "kind": "port",
             "sample": f"{n} packets of the same workload, seal+open, {reps} reps, oracle/liboracle.so "
                       f"(-O3, bit-exact restatement of the reference C path)",
             "seal": round(m_seal, 3), "open": round(m_open, 3),

@@ -42,6 +42,11 @@ extern "C" {
 #define WG_EDEVICE (-5)    /* HIP runtime error (message via wg_last_error) */
 #define WG_ESELFTEST (-74) /* known-answer self test failed */
 #define WG_EAGAIN (-11)    /* wg_submit_*: no free queue slot within the queue's submit timeout */
+/* wg_seal1 / wg_open1 / wg_submit_*: the key slot holds no key (never set, or zeroed by wg_keys_zero).
+ * SymmetricKeypair.clean() closes its key arena, so a later cipher() / decipher() throws instead of
+ * encrypting (SymmetricKeypair.java:85-93); these paths refuse the packet the same way rather than
+ * sealing it under the publicly known all-zero key. */
+#define WG_ENOKEY (-126)
 
 #define WG_PKT_OK 0u
 #define WG_PKT_BADTAG 1u
@@ -51,6 +56,9 @@ extern "C" {
 #define WG_PKT_BADIP 4u     /* IP version nibble not 4 or 6, or too short for the destination address */
 #define WG_PKT_FILTERED 5u  /* destination outside the key slot's AllowedIPs filter */
 #define WG_PKT_REPLAY 6u    /* counter replayed, too old for the window, or >= 2^64 - 2^13 - 1 */
+/* a queued packet whose key slot was zeroed between its submit's check and its copy into the ring:
+ * never sealed or opened (its output is untouched) */
+#define WG_PKT_NOKEY 7u
 /* a queued packet (wg_submit_*) whose batch could not run (launch or stream error) */
 #define WG_PKT_FAILED 255u
 
@@ -364,7 +372,8 @@ int wg_open_host(wg_ctx* ctx, const wg_pkt* desc_host, uint32_t n, const uint8_t
  *     and queues it; the nonce is LE64(counter) || 0^4 (SymmetricKeypair.java:52-61), the key
  *     the one key_slot holds at the time of the submit (copied into the slot with the packet, as the
  *     reference's synchronous cipher() uses the key it holds when called: a later wg_keys_set /
- *     wg_keys_zero of the slot does not change a queued packet). Blocks only while every slot is in
+ *     wg_keys_zero of the slot does not change a queued packet; the copy is wiped when the packet's
+ *     batch completes). A slot without a key (never set, or zeroed) is refused: WG_ENOKEY. Blocks only while every slot is in
  *     use (until the consumer calls wg_reap_done), and then at most the queue's submit timeout:
  *     returns WG_EAGAIN after it. Thread-safe: any number of producers.
  *   wg_submit_open(q, key_slot, counter, ct_tag, len, user): the same for ct || tag (len + 16 B).
@@ -396,7 +405,7 @@ typedef struct wg_completion {
   uint64_t counter;
   uint8_t* data;      /* result in the pinned ring (see above) */
   uint32_t len;       /* payload bytes */
-  uint32_t status;    /* WG_PKT_OK, WG_PKT_BADTAG (open) or WG_PKT_FAILED */
+  uint32_t status;    /* WG_PKT_OK, WG_PKT_BADTAG (open), WG_PKT_NOKEY or WG_PKT_FAILED */
   uint32_t key_slot;
   uint32_t slot;      /* ring slot (handed back by wg_reap_done) */
   uint64_t submit_ns; /* steady-clock time of the submit (latency accounting) */
@@ -419,6 +428,10 @@ int wg_reap(wg_queue* q, wg_completion* out, uint32_t max, uint32_t timeout_us);
 int wg_reap_done(wg_queue* q, const wg_completion* done, uint32_t n);
 int wg_queue_stats(wg_queue* q, uint64_t* batches, uint64_t* packets);
 int wg_queue_set_submit_timeout(wg_queue* q, uint32_t timeout_us);
+/* Diagnostic: ring slots whose copy of a session key is not all zero. A slot's key copy is wiped as
+ * soon as its batch has completed, so with nothing in flight this is 0 (no key outlives the packets
+ * that used it in pinned memory, as clean() leaves none, SymmetricKeypair.java:85-89). */
+uint32_t wg_queue_key_residue(const wg_queue* q);
 
 /* Pinned host rings for the host path (the reference's packet buffers come from
  * a native pool, Pool.java:96; pinning them makes wg_seal_host/wg_open_host zero-copy).

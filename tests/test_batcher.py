@@ -125,7 +125,15 @@ def test_per_packet_edges_bit_exact():
         pt = splitmix_bytes(1803, 700)
         assert eng.seal1(1, 5, pt) == O.c_aead_seal(k_new, O.transport_nonce(5), pt)
         eng.zero_keys(1, 1)
-        assert eng.seal1(1, 6, pt) == O.c_aead_seal(bytes(32), O.transport_nonce(6), pt)
+        # clean(): the next call is refused, never sealed under the all-zero key (the
+        # reference's cipher() throws once the key arena is closed, SymmetricKeypair.java:85-93)
+        for fn, data in ((eng.seal1, pt), (eng.open1, pt + bytes(16))):
+            for big in (False, True):  # a ring slot, and the host batch path past it
+                with pytest.raises(W.WgError) as ei:
+                    fn(1, 6, data if not big else data * 8)
+                assert ei.value.code == W._lib.WG_ENOKEY
+        eng.set_keys(1, k_new)
+        assert eng.seal1(1, 6, pt) == O.c_aead_seal(k_new, O.transport_nonce(6), pt)
         # forged tag: return 1, dst untouched
         lib = W.lib()
         for L in (100, 5000):

@@ -81,3 +81,26 @@ def test_desc_packing_matches_c_layout():
     assert q.shape == (2, 4)
     assert q[0].tolist() == [1, 3, 5, 1420 | (7 << 32)]
     assert np.uint64(q[1, 2].view(np.uint64)) == np.uint64((1 << 64) - 1)
+
+
+def test_fault_hooks_only_in_the_test_library():
+    """the product library must not read the fault-injection variables (WG_TEST_STEP_FLIP makes
+    k_step write wrong tags, WG_RX_TEST_MUTANT restores a racy replay flag). They are compiled only into
+    libwgaead_test.so (-DWG_TEST_HOOKS), which the tests needing them load through WG_LIB_PATH."""
+    here = os.path.join(ROOT, "wireguard-java_amd")
+    prod = open(os.path.join(here, "libwgaead.so"), "rb").read()
+    for hook in (b"WG_TEST_STEP_FLIP", b"WG_RX_TEST_SKEW", b"WG_RX_TEST_MUTANT"):
+        assert hook not in prod, hook
+    test_lib = os.path.join(here, "libwgaead_test.so")
+    assert os.path.exists(test_lib), "make -C wireguard-java_amd/csrc test"
+    t = open(test_lib, "rb").read()
+    for hook in (b"WG_TEST_STEP_FLIP", b"WG_RX_TEST_SKEW", b"WG_RX_TEST_MUTANT"):
+        assert hook in t, hook
+
+
+def test_no_key_codes_declared():
+    """WG_ENOKEY / WG_PKT_NOKEY: the per-packet and queue paths refuse a key slot without a key."""
+    L = wg()._lib
+    src = open(HEADER).read()
+    assert f"#define WG_ENOKEY ({L.WG_ENOKEY})" in src
+    assert f"#define WG_PKT_NOKEY {L.WG_PKT_NOKEY}u" in src

@@ -80,7 +80,11 @@ def test_bench_line_fails_when_k_step_writes_a_wrong_tag():
     """WG_TEST_STEP_FLIP=64: k_step flips one tag bit of every 64th packet between its seal and open
     halves. The bench line must then report verified false and oracle_sample.bit_exact false, and the
     bench must exit 3. Without the hook the same short run is verified and bit-exact."""
-    rc, line = _bench({"WG_TEST_STEP_FLIP": "64"})
+    # the hook exists only in the test library (make -C wireguard-java_amd/csrc test); the product
+    # library ignores the variable (ADVICE r5), which the last run below also shows
+    test_lib = os.path.join(ROOT, "wireguard-java_amd", "libwgaead_test.so")
+    assert os.path.exists(test_lib), "build the test library first (__graft_entry__.build())"
+    rc, line = _bench({"WG_TEST_STEP_FLIP": "64", "WG_LIB_PATH": test_lib})
     assert rc == 3, line
     assert line["verified"] is False
     assert line["oracle_sample"]["bit_exact"] is False
@@ -88,3 +92,5 @@ def test_bench_line_fails_when_k_step_writes_a_wrong_tag():
     assert rc == 0, line
     assert line["verified"] is True and line["oracle_sample"]["bit_exact"] is True
     assert line["config"]["streams"] == 2 and line["roofline"]["kernel_names"] == ["k_step"]
+    rc, line = _bench({"WG_TEST_STEP_FLIP": "64"})  # the product library: no hook, still bit-exact
+    assert rc == 0 and line["verified"] is True and line["oracle_sample"]["bit_exact"] is True

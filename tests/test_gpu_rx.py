@@ -405,37 +405,20 @@ def test_rx_argument_contract(engine):
     assert lib.wg_filter_set(engine.ctx, W._lib.WG_MAX_FILTERS, None, 0) == W._lib.WG_ERANGE
 
 
-@pytest.mark.parametrize("mutant", [False, True])
-def test_replay_flag_protocol_under_block_skew(mutant):
-    """Regression test of the order-flag race fixed in round 4 (98a2832): k_rp_fixmark cleared the
-    order flag that its own later-starting blocks still read, so they skipped their duplicate
-    fix-ups and a repeated (slot, counter) could be accepted twice. WG_RX_TEST_SKEW delays every
-    block but block 0 of each replay launch by 30 us, so block 0 always finishes first.
-    Consecutive duplicate-laden checks must then still match the oracle (flag words, done counts,
-    group counts and new-top copies all read after the skew). WG_RX_TEST_MUTANT=1 puts the old flag
-    clearing back: the same checks must then disagree with the oracle, which shows that the skew
-    exposes the race. Reference: TransportManager.java:98-119 (the window itself is unpinned)."""
-    import os
+def _skew_check(mutant: bool) -> dict:
+    """Body of test_replay_flag_protocol_under_block_skew, run in a child process that loads the test
+    library (the hooks exist only there) with the hook variables set: four duplicate-laden replay
+    checks, each compared with the oracle (statuses and every slot's window)."""
     torch, dev = _dev()
     W = wg()
-    env = {"WG_RX_LAUNCHES": "3", "WG_RX_TEST_SKEW": "30", "WG_RX_TEST_MUTANT": "1" if mutant else "0"}
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
-        engine = W.Engine(0, key_slots=512)
-        engine.replay_enable(256)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
+    engine = W.Engine(0, key_slots=512)
+    engine.replay_enable(256)
     try:
         engine.set_keys(0, splitmix_np(9, 32 * 16).tobytes())
         o = rx.ReplayWindow(256)
         rng = np.random.default_rng(77)
         base = np.zeros(16, np.int64)
-        agree = []
+        agree, replays = [], []
         for b in range(4):
             n = 20000  # 79 blocks
             slots = rng.integers(0, 16, n)
@@ -452,11 +435,43 @@ def test_replay_flag_protocol_under_block_skew(mutant):
                 top, words = engine.replay_state(s_, 256)
                 otop, owords = o.bitmap(s_)
                 same = same and top == otop and [int(x) for x in words] == owords
-            agree.append(same)
-            if not mutant:
-                assert same, b
-                assert any(x == rx.PKT_REPLAY for x in want)
-        if mutant:
-            assert not all(agree), "the skew did not expose the round-4 flag race"
+            agree.append(bool(same))
+            replays.append(any(x == rx.PKT_REPLAY for x in want))
+        return {"agree": agree, "replays": replays, "lib": W._lib.LIB_PATH}
     finally:
         engine.close()
+
+
+@pytest.mark.parametrize("mutant", [False, True])
+def test_replay_flag_protocol_under_block_skew(mutant):
+    """Regression test of the order-flag race fixed in round 4 (98a2832): k_rp_fixmark cleared the
+    order flag that its own later-starting blocks still read, so they skipped their duplicate
+    fix-ups and a repeated (slot, counter) could be accepted twice. WG_RX_TEST_SKEW delays every
+    block but block 0 of each replay launch by 30 us, so block 0 always finishes first.
+    Consecutive duplicate-laden checks must then still match the oracle (flag words, done counts,
+    group counts and new-top copies all read after the skew). WG_RX_TEST_MUTANT=1 puts the old flag
+    clearing back: the same checks must then disagree with the oracle, which shows that the skew
+    exposes the race. The hooks exist only in the test library, so the check runs in a
+    child process that loads it. Reference: TransportManager.java:98-119 (the window itself is unpinned)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    test_lib = os.path.join(root, "wireguard-java_amd", "libwgaead_test.so")
+    assert os.path.exists(test_lib), "build the test library first (__graft_entry__.build())"
+    env = dict(os.environ, WG_LIB_PATH=test_lib, WG_RX_LAUNCHES="3", WG_RX_TEST_SKEW="30",
+               WG_RX_TEST_MUTANT="1" if mutant else "0")
+    code = ("import json, sys; sys.path[:0] = ['tests', '.']; import test_gpu_rx as t; "
+            f"print(json.dumps(t._skew_check({bool(mutant)})), flush=True)")
+    p = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=100)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and lines, p.stderr[-2000:]
+    r = json.loads(lines[-1])
+    assert r["lib"] == test_lib
+    if mutant:
+        assert not all(r["agree"]), "the skew did not expose the round-4 flag race"
+    else:
+        assert all(r["agree"]), r
+        assert all(r["replays"])
+

@@ -206,16 +206,27 @@ def test_queued_packets_keep_the_key_they_were_submitted_with():
             q.submit(1, i, pts[i], i)
         eng.zero_keys(1, 1)  # clean(): the queued packets keep k_old
         for i in range(20, 30):
-            q.submit(1, i, pts[i], i)  # submitted after the zeroing: the zero key, as wg_seal1 would
+            # submitted after the zeroing: refused (sealing under the all-zero key was fail-open;
+            # the reference's cipher() throws once clean() has closed the key arena)
+            with pytest.raises(W.WgError) as ei:
+                q.submit(1, i, pts[i], i)
+            assert ei.value.code == W._lib.WG_ENOKEY
+        with pytest.raises(W.WgError) as ei:  # a batched submit with one such entry queues nothing
+            q.submit_n([(1, 20, pts[20], 20)])
+        assert ei.value.code == W._lib.WG_ENOKEY
         eng.set_keys(1, k_new)
         for i in range(30, 40):
             q.submit(1, i, pts[i], i)
-        got = _reap_all(q, 40)
-        for i in range(40):
-            key = k_old if i < 20 else bytes(32) if i < 30 else k_new
+        got = _reap_all(q, 30)
+        assert sorted(got) == list(range(20)) + list(range(30, 40))
+        for i in got:
+            key = k_old if i < 20 else k_new
             ctr, st, data = got[i]
             assert st == 0 and ctr == i
             assert data == O.c_aead_seal(key, O.transport_nonce(i), pts[i]), i
+        # every completed batch's key copies are wiped from the pinned ring (they stayed until
+        # the queue was freed, so a zeroed session's key outlived clean() in pinned memory)
+        assert W._lib.wg_queue_key_residue(q.q) == 0
     finally:
         if q is not None:
             q.close()
@@ -467,3 +478,36 @@ def test_queue_argument_contract():
     assert lib.wg_queue_stats(None, None, None) == E
     assert lib.wg_queue_set_submit_timeout(None, 0) == E
     assert lib.wg_queue_destroy(None) == 0
+
+
+@pytest.mark.gpu
+def test_no_key_left_in_the_ring_after_reap():
+    """After a batch completes, its slots' key copies are zeroed: keys_zero followed by a reap leaves no
+    key bytes in the queue's pinned key ring (SymmetricKeypair.clean zeroes its keys,
+    SymmetricKeypair.java:85-89). A slot that never held a key is refused as well."""
+    W = wg()
+    eng = W.Engine(0, key_slots=4)
+    q = None
+    try:
+        eng.set_keys(0, splitmix_bytes(2601, 64))
+        for mode in ("seal", "open"):
+            q = eng.queue(mode, capacity=256)
+            extra = 16 if mode == "open" else 0
+            for i in range(200):
+                q.submit(i % 2, i, splitmix_bytes(2700 + i, 64 + i + extra), i)
+            eng.zero_keys(0, 1)
+            got = _reap_all(q, 200)
+            assert len(got) == 200
+            if mode == "seal":
+                assert all(st == 0 for _, st, _ in got.values())
+            assert W._lib.wg_queue_key_residue(q.q) == 0
+            with pytest.raises(W.WgError) as ei:
+                q.submit(2, 0, b"x" * (8 + extra), 0)  # never set
+            assert ei.value.code == W._lib.WG_ENOKEY
+            q.close()
+            q = None
+            eng.set_keys(0, splitmix_bytes(2602, 32))
+    finally:
+        if q is not None:
+            q.close()
+        eng.close()

@@ -16,6 +16,10 @@ PART=${2:-all}
 step() { echo "[round] $1"; }
 die() { echo "[round] FAILED: $1 (rc $2)"; exit $2; }
 if [ "$PART" != prof ]; then
+step "build on the box (every library the tests and the bench load comes from this tree's sources)"
+timeout -k 10 400 python -c "import __graft_entry__ as g; g.build()" > $O/build.log 2>&1 || die build $?
+md5sum wireguard-java_amd/libwgaead.so wireguard-java_amd/libwgaead_test.so oracle/liboracle.so > $O/build_md5.txt
+git_head=$(cat .git_head 2>/dev/null || echo unknown); echo "head $git_head" >> $O/build_md5.txt
 step tests
 timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 || die tests $?
 tail -1 $O/gpu_tests.log
@@ -54,11 +58,6 @@ timeout -k 10 300 ./tools/host_pipeline --backend cpu --oracle oracle/liboracle.
 step "receive side"
 timeout -k 10 180 python tools/bench_rx.py > $O/rx_timing.json || die rx $?
 cat $O/rx_timing.json
-step "per-packet server"
-for t in 1 16 64; do timeout -k 10 120 ./tools/batcher_bench $t $((t == 1 ? 4000 : 160000 / t)) 1420 >> $O/batcher.jsonl || die batcher $?; done
-timeout -k 10 120 ./tools/batcher_bench 16 10000 0 >> $O/batcher.jsonl || die batcher_mixed $?
-cat $O/batcher.jsonl
-timeout -k 10 120 ./tools/pp_stamps 1420 > $O/pp_stamps.json || die pp_stamps $?
 fi
 [ "$PART" = bench ] && { step done; exit 0; }
 cd /tmp && export TMPDIR=/tmp

@@ -21,6 +21,7 @@ WG_E2BIG = -7
 WG_EDEVICE = -5
 WG_ESELFTEST = -74
 WG_EAGAIN = -11
+WG_ENOKEY = -126
 WG_PKT_OK = 0
 WG_PKT_BADTAG = 1
 WG_PKT_BADHDR = 2
@@ -28,6 +29,7 @@ WG_PKT_KEEPALIVE = 3
 WG_PKT_BADIP = 4
 WG_PKT_FILTERED = 5
 WG_PKT_REPLAY = 6
+WG_PKT_NOKEY = 7
 WG_PKT_FAILED = 255
 WG_QUEUE_MAX_LEN = 16384
 WG_RX_FILTER = 1
@@ -46,7 +48,7 @@ WG_F_RX_FILTER = 8
 WG_MODE_SEAL, WG_MODE_OPEN, WG_MODE_CIPHER, WG_MODE_MAC = 0, 1, 2, 3
 
 _ERRNAMES = {WG_EINVAL: "EINVAL", WG_ENOMEM: "ENOMEM", WG_ERANGE: "ERANGE", WG_E2BIG: "E2BIG",
-             WG_EDEVICE: "EDEVICE", WG_ESELFTEST: "ESELFTEST", WG_EAGAIN: "EAGAIN"}
+             WG_EDEVICE: "EDEVICE", WG_ESELFTEST: "ESELFTEST", WG_EAGAIN: "EAGAIN", WG_ENOKEY: "ENOKEY"}
 
 
 class WgError(RuntimeError):
@@ -142,6 +144,7 @@ SIGNATURES = [
     ("wg_reap_done", _I, [_VP, ctypes.POINTER(WgCompletion), _U32]),
     ("wg_queue_stats", _I, [_VP, ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
     ("wg_queue_set_submit_timeout", _I, [_VP, _U32]),
+    ("wg_queue_key_residue", _U32, [_VP]),
     ("wg_seal_host", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _U32, _U32]),
     ("wg_open_host", _I, [_VP, _VP, _U32, _VP, _U64, _VP, _U64, _VP, _U32, _U32]),
     ("wg_host_alloc", _I, [_VP, _U64, ctypes.POINTER(_VP)]),

@@ -142,6 +142,11 @@ struct wg_ctx {
   // serialise on keys_mu. key_snapshot() reads a consistent key.
   std::unique_ptr<std::atomic<uint64_t>[]> key_words;
   std::unique_ptr<std::atomic<uint32_t>[]> key_seq;  // even: stable, odd: being written
+  // per slot: 1 once wg_keys_set wrote a key, 0 when never set or zeroed by wg_keys_zero (clean()): the
+  // paths that carry a key with the packet refuse a packet for a slot without a key (WG_ENOKEY /
+  // WG_PKT_NOKEY) instead of sealing it under the all-zero key, as the reference's cipher() / decipher()
+  // throw once clean() has closed the key arena (SymmetricKeypair.java:85-93)
+  std::unique_ptr<std::atomic<uint32_t>[]> key_live;
   std::mutex keys_mu;
   RxState* rx = nullptr;  // receive-side checks (wg_rx.hip)
   // timing
@@ -166,7 +171,8 @@ struct DeviceGuard {
 
 // The key of `slot` as the host mirror holds it now (sequence-lock read: retried while a writer is
 // inside wg_keys_set / wg_keys_zero for that slot, so the 32 bytes are never a mix of two keys).
-void key_snapshot(const wg_ctx* c, uint32_t slot, uint32_t key[8]) {
+// Returns whether the slot holds a key (false: never set, or zeroed; `key` is then all zero).
+bool key_snapshot(const wg_ctx* c, uint32_t slot, uint32_t key[8]) {
   std::atomic<uint32_t>& sq = c->key_seq[slot];
   for (;;) {
     const uint32_t s1 = sq.load(std::memory_order_acquire);
@@ -176,13 +182,17 @@ void key_snapshot(const wg_ctx* c, uint32_t slot, uint32_t key[8]) {
     }
     uint64_t w[4];
     for (int i = 0; i < 4; ++i) w[i] = c->key_words[4u * slot + i].load(std::memory_order_relaxed);
+    const uint32_t live = c->key_live[slot].load(std::memory_order_relaxed);
     std::atomic_thread_fence(std::memory_order_acquire);
     if (sq.load(std::memory_order_relaxed) == s1) {
       memcpy(key, w, 32);
-      return;
+      return live != 0;
     }
   }
 }
+
+// Whether `slot` holds a key now (the up-front check of a per-packet call or a queue submit).
+bool key_is_live(const wg_ctx* c, uint32_t slot) { return c->key_live[slot].load(std::memory_order_acquire) != 0; }
 
 // Writes slots [first, first + n) of the host mirror (keys: n x 32 B, or NULL for zeros). Caller holds
 // c->keys_mu.
@@ -195,6 +205,7 @@ void key_mirror_write(wg_ctx* c, uint32_t first, uint32_t n, const uint8_t* keys
     uint64_t w[4] = {0, 0, 0, 0};
     if (keys) memcpy(w, keys + 32ull * k, 32);
     for (int i = 0; i < 4; ++i) c->key_words[4ull * (first + k) + i].store(w[i], std::memory_order_relaxed);
+    c->key_live[first + k].store(keys ? 1u : 0u, std::memory_order_relaxed);
     sq.store(s0 + 2u, std::memory_order_release);
   }
 }
@@ -665,8 +676,10 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
       if (claim_nc) hipLaunchKernelGGL((wgt::k_step_claim<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else if (PS.n_long && sp.gs == 4) hipLaunchKernelGGL(wgt::k_step_mixed<4>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else if (PS.n_long) hipLaunchKernelGGL(wgt::k_step_mixed<8>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+#ifdef WG_TEST_HOOKS
       else if (c->test_flip && G == 8)  // test hook build: the same body with the tag flip between the halves
         hipLaunchKernelGGL((wgt::k_step<8, 4, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, c->test_flip);
+#endif
       else if (G == 16) hipLaunchKernelGGL(wgt::k_step<16>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
       else if (G == 4) hipLaunchKernelGGL(wgt::k_step<4>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
       else if (c->step_wpe4 && 2ull * gs * wgt::TW <= cap)
@@ -768,6 +781,7 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   }
   c->key_words.reset(new std::atomic<uint64_t>[(size_t)key_slots * 4]());
   c->key_seq.reset(new std::atomic<uint32_t>[key_slots]());
+  c->key_live.reset(new std::atomic<uint32_t>[key_slots]());
   c->cus = (uint32_t)prop.multiProcessorCount;
   for (int w = 0; w < 3; ++w)
     for (int k = 0; k < 3; ++k)
@@ -787,10 +801,14 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   if (const char* e = getenv("WG_PRIO")) c->prio_mode = atoi(e);
   if (const char* e = getenv("WG_STEP_WPE4")) c->step_wpe4 = atoi(e) != 0;
   if (const char* e = getenv("WG_CLAIM")) c->claim = atoi(e) != 0;
+#ifdef WG_TEST_HOOKS
+  // fault-injection hooks exist only in the test library (make test: libwgaead_test.so); the product
+  // library never reads these variables, so no environment can make it write wrong tags
   if (const char* e = getenv("WG_TEST_STEP_FLIP")) {
     const long v = atol(e);
     c->test_flip = (v > 0 && (v & (v - 1)) == 0) ? (uint32_t)v : 0u;
   }
+#endif
   *out = c;
   return WG_OK;
 }

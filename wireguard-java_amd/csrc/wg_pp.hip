@@ -396,10 +396,16 @@ __device__ void pp_serve(Unit& U, const PPParams& P, uint32_t i, uint64_t t_seen
   if (tid == 0) {
     // the service time first (only with WG_PP_CALL_STAMPS: one more PCIe write per packet): it is
     // ordered before the completion word the caller polls for
-    if (P.svc)
+    if (P.svc) {
       __hip_atomic_store(P.svc + i, __builtin_amdgcn_s_memrealtime() - t_seen, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(P.done + i, (seq << 8) | status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      // two relaxed stores to different addresses are not ordered by the memory model: the completion
+      // word is stored with release semantics below, so a caller that sees it also sees this value
+    }
+    if (P.svc)
+      __hip_atomic_store(P.done + i, (seq << 8) | status, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    else
+      __hip_atomic_store(P.done + i, (seq << 8) | status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -895,6 +901,9 @@ int pp_sleep(PPServer* S, uint32_t i, uint64_t seq, uint64_t* d_out) {
 
 int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const uint8_t* src, uint32_t len,
               uint8_t* dst) {
+  // a slot without a key (never set, or zeroed by wg_keys_zero = clean()): refused, not sealed or opened
+  // under the all-zero key (the reference's cipher() / decipher() throw once clean() closed the arena)
+  if (!key_is_live(c, key_slot)) return fail(WG_ENOKEY, "key slot %u holds no key (zeroed or never set)", key_slot);
   if (len > wgpp::kPPMaxLen) return pp_big(c, open, key_slot, counter, src, len, dst);
   PPServer* S;
   int rc;
@@ -906,7 +915,8 @@ int pp_submit(wg_ctx* c, bool open, uint32_t key_slot, uint64_t counter, const u
   st = PPCallStamps{};
   if (stamp) st.t_enter = pp_now_ns();
   uint32_t key[8];
-  key_snapshot(c, key_slot, key);
+  if (!key_snapshot(c, key_slot, key))  // zeroed since the check above
+    return fail(WG_ENOKEY, "key slot %u holds no key (zeroed or never set)", key_slot);
   if (t_pp.server != (const void*)S) {
     t_pp.server = S;
     t_pp.wave = S->threads.fetch_add(1, std::memory_order_relaxed);

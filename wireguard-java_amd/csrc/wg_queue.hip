@@ -153,7 +153,7 @@ struct SlotMeta {  // written by the producer before the slot id is pushed
   uint32_t len;
   uint32_t key_slot;
   uint32_t status;  // set by the dispatcher when the batch completes
-  uint32_t _pad;
+  uint32_t nokey;   // the key slot was zeroed between the submit's check and the copy: never sealed / opened
 };
 
 struct Batch {  // one in-flight launch
@@ -214,7 +214,9 @@ struct wg_queue {
   // sealed or opened with, exactly as a synchronous cipher() before clean() used the old key.
   uint32_t* h_key = nullptr;
   uint32_t* z_key = nullptr;
-  uint64_t submit_timeout_ns = 0;  // wg_queue_set_submit_timeout: 0 = a submit waits for a free slot without bound
+  // wg_queue_set_submit_timeout: 0 = a submit waits for a free slot without bound (set from any thread
+  // while producers read it)
+  std::atomic<uint64_t> submit_timeout_ns{0};
   std::unique_ptr<wgq::SlotMeta[]> meta;
   wgq::IdQueue done_q;                // completions: pushed by the dispatcher, popped by consumers
   uint32_t lanes = 0, per_lane = 0;     // producer lanes and the ring slots each owns
@@ -266,7 +268,12 @@ int queue_launch(wg_queue* q, wgq::Batch& b, uint32_t lmax) {
 void queue_complete(wg_queue* q, wgq::Batch& b, uint32_t status_override) {
   for (uint32_t j = 0; j < b.n; ++j) {
     const uint32_t s = b.slots[j];
-    q->meta[s].status = status_override != 0 ? status_override
+    // the batch's event has completed (or it never ran): no launch reads this slot's key copy any more,
+    // so it is wiped now rather than when the queue is freed (SymmetricKeypair.clean zeroes its keys,
+    // SymmetricKeypair.java:85-89; the per-packet path wipes its copy after each call the same way)
+    memset(q->h_key + 8ull * s, 0, 32);
+    q->meta[s].status = q->meta[s].nokey ? (uint32_t)WG_PKT_NOKEY
+                        : status_override != 0 ? status_override
                         : q->mode == WG_MODE_OPEN ? b.h_status[j] : (uint32_t)WG_PKT_OK;
     while (!q->done_q.push(s)) std::this_thread::yield();  // cannot stay full: it holds at most cap ids
   }
@@ -326,11 +333,11 @@ void queue_dispatch(wg_queue* q) {
           d.in_off = (uint64_t)s * q->stride;
           d.out_off = (uint64_t)s * q->stride;
           d.counter = m.counter;
-          d.len = m.len;
+          d.len = m.nokey ? WG_LEN_INVALID : m.len;  // no key: the kernel skips the packet (out of range)
           d.key_slot = s;  // the key copied into the ring slot at submit time
           if (fill->n == 0) first_ns = wgq::now_ns();
           fill->slots[fill->n++] = s;
-          lmax = std::max(lmax, m.len);
+          if (!m.nokey) lmax = std::max(lmax, m.len);
         }
         ln.r_head.store(h, std::memory_order_relaxed);
       }
@@ -452,12 +459,12 @@ int queue_acquire(wg_queue* q, wgq::Lane& ln, uint32_t* s, uint64_t* deadline) {
     const uint32_t w = q->wake_word.load(std::memory_order_acquire);
     const int r = queue_try_slot(q, ln, s);
     if (r == 1) return WG_OK;
-    if (q->submit_timeout_ns) {
+    if (const uint64_t tmo = q->submit_timeout_ns.load(std::memory_order_relaxed)) {
       const uint64_t now = wgq::now_ns();
-      if (!*deadline) *deadline = now + q->submit_timeout_ns;
+      if (!*deadline) *deadline = now + tmo;
       else if (now >= *deadline)
         return fail(WG_EAGAIN, "no free queue slot for %llu us (is the consumer calling wg_reap_done?)",
-                    (unsigned long long)(q->submit_timeout_ns / 1000u));
+                    (unsigned long long)(tmo / 1000u));
     }
     // this lane's ready ring is full (the dispatcher is about to gather it), or every slot is in use:
     // wait for wg_reap_done without burning the CPU the consumers need to free them
@@ -477,11 +484,13 @@ int queue_acquire(wg_queue* q, wgq::Lane& ln, uint32_t* s, uint64_t* deadline) {
   }
 }
 
-// Fill slot s with one packet: its key as the key slot holds it now, its meta, its bytes.
+// Fill slot s with one packet: its key as the key slot holds it now, its meta, its bytes. A key slot
+// zeroed since queue_check_packet (a clean() racing the submit) marks the packet: it completes with
+// WG_PKT_NOKEY and is never sealed or opened under the zero key.
 void queue_fill(wg_queue* q, uint32_t s, uint32_t key_slot, uint64_t counter, const uint8_t* src, uint32_t len,
                 uint64_t user) {
-  key_snapshot(q->c, key_slot, q->h_key + 8ull * s);
   wgq::SlotMeta& m = q->meta[s];
+  m.nokey = key_snapshot(q->c, key_slot, q->h_key + 8ull * s) ? 0u : 1u;
   m.user = user;
   m.counter = counter;
   m.len = len;
@@ -515,6 +524,7 @@ int queue_check_packet(wg_queue* q, int mode, uint32_t key_slot, const uint8_t* 
   if (!src && (len || mode == WG_MODE_OPEN)) return fail(WG_EINVAL, "NULL argument");
   if (len > q->max_len) return fail(WG_E2BIG, "packet of %u bytes > the queue's max_len %u", len, q->max_len);
   if (key_slot >= q->c->key_slots) return fail(WG_ERANGE, "key slot %u", key_slot);
+  if (!key_is_live(q->c, key_slot)) return fail(WG_ENOKEY, "key slot %u holds no key (zeroed or never set)", key_slot);
   return WG_OK;
 }
 
@@ -786,8 +796,19 @@ int wg_reap_done(wg_queue* q, const wg_completion* done, uint32_t n) {
 
 int wg_queue_set_submit_timeout(wg_queue* q, uint32_t timeout_us) {
   if (!q) return fail(WG_EINVAL, "NULL queue");
-  q->submit_timeout_ns = 1000ull * timeout_us;
+  q->submit_timeout_ns.store(1000ull * timeout_us, std::memory_order_relaxed);
   return WG_OK;
+}
+
+uint32_t wg_queue_key_residue(const wg_queue* q) {
+  if (!q) return 0;
+  uint32_t n = 0;
+  for (uint32_t s = 0; s < q->cap; ++s) {
+    uint32_t any = 0;
+    for (uint32_t k = 0; k < 8u; ++k) any |= ((const volatile uint32_t*)q->h_key)[8ull * s + k];
+    n += any ? 1u : 0u;
+  }
+  return n;
 }
 
 int wg_queue_stats(wg_queue* q, uint64_t* batches, uint64_t* packets) {

@@ -128,8 +128,10 @@ int rx_get(wg_ctx* c, RxState** out) {
   if (!c->rx) {
     c->rx = new RxState();
     if (const char* e = getenv("WG_RX_LAUNCHES")) c->rx->five = atoi(e) == 5;
+#ifdef WG_TEST_HOOKS  // the test library only (libwgaead_test.so): never read by the product library
     if (const char* e = getenv("WG_RX_TEST_SKEW")) c->rx->test_skew_ticks = 100u * (uint32_t)std::max(0, atoi(e));
     if (const char* e = getenv("WG_RX_TEST_MUTANT")) c->rx->test_mutant = atoi(e) != 0;
+#endif
   }
   *out = c->rx;
   return WG_OK;
@@ -228,6 +230,9 @@ struct RxParams {
 // check's shared words, so block 0 runs its whole part first. A protocol in which an early block
 // clears or consumes a word a later block of the same launch still reads then fails every time.
 __device__ __forceinline__ void rx_test_skew(const RxParams& P) {
+#ifndef WG_TEST_HOOKS
+  return;  // the product library carries no skew code
+#endif
   if (P.skew_ticks == 0u || blockIdx.x == 0u) return;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)P.skew_ticks) __builtin_amdgcn_s_sleep(8);
@@ -598,7 +603,11 @@ __global__ void __launch_bounds__(256) k_rp_fixmark(RxParams P) {
   if (own_entry) P.tab[P.pos[i]] = ~0u;
   // the next check's flag, not this one's: every thread of this launch reads this check's flag, and
   // a block that starts after thread 0 has cleared it would skip its fix-ups
+#ifdef WG_TEST_HOOKS
   if (i == 0) reset_word(P.mutant ? P.unsorted : P.unsorted_next);
+#else
+  if (i == 0) reset_word(P.unsorted_next);
+#endif
 }
 __global__ void __launch_bounds__(256) k_rp_mark(RxParams P) {
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;

@@ -948,7 +948,8 @@ __device__ __forceinline__ void step_test_flip(const TransportParams& S, uint32_
   asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
 }
 
-// FLIP: the test-hook build (WG_TEST_STEP_FLIP); the product instantiations carry no hook code at all.
+// FLIP: the test-hook instantiation (WG_TEST_STEP_FLIP), launched only by the test library (WG_TEST_HOOKS);
+// the product instantiations carry no hook code at all.
 template <int G = 8, int WPE = 8, bool FLIP = false>
 __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_step(TransportParams S, TransportParams O, uint32_t test_flip) {
