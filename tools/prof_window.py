@@ -36,6 +36,9 @@ def window(b):
     # a K-stream step (bench.py --streams K > 1) cuts the batch into K runs, one launch each
     st = b["roofline"].get("step") or {}
     per = st["launches"] if st.get("streams", 1) > 1 else b["roofline"].get("launches_per_step", 1)
+    if b.get("launches_before_window") is not None and b.get("window_launches") is not None:
+        # bench.py counts its transport launches (a staggered two-stream schedule has one more per run)
+        return b["launches_before_window"], b["window_launches"], per
     skip = (b["ramp_steps"] + b["warmup"] + b.get("graph_warm_steps", 0)) * per
     return skip, b["steps"] * per, per
 

@@ -36,13 +36,19 @@ def main():
         raise SystemExit(f"window needs {count} dispatches after {skip}, trace has {len(rows)}")
     t0 = min(int(r["Start_Timestamp"]) for r in win)
     steps = []
-    for s in range(b["steps"]):
+    for s in range(min(b["steps"], len(win) // per)):
         d = win[s * per:(s + 1) * per]
         st_ = [(int(r["Start_Timestamp"]) - t0) / 1e3 for r in d]
         en_ = [(int(r["End_Timestamp"]) - t0) / 1e3 for r in d]
         steps.append({"step": s, "queues": [r["Queue_Id"] for r in d], "start_us": st_, "end_us": en_,
                       "dur_us": [e - x for x, e in zip(st_, en_)],
                       "start_offset_us": (max(st_) - min(st_)) if per > 1 else 0.0})
+    # per stream (queue): its launches back to back, first start and last end
+    by_q = {}
+    for r in win:
+        by_q.setdefault(r["Queue_Id"], []).append(((int(r["Start_Timestamp"]) - t0) / 1e3, (int(r["End_Timestamp"]) - t0) / 1e3))
+    streams = {q: {"launches": len(v), "first_start_us": round(min(x for x, _ in v), 2),
+                   "last_end_us": round(max(e for _, e in v), 2)} for q, v in by_q.items()}
     span = (max(int(r["End_Timestamp"]) for r in win) - t0) / 1e3
     offs = [x["start_offset_us"] for x in steps]
     durs = [d for x in steps for d in x["dur_us"]]
@@ -51,7 +57,7 @@ def main():
            "launch_dur_mean_us": round(st.mean(durs), 2),
            "start_offset_first5_us": [round(o, 2) for o in offs[:5]],
            "start_offset_last5_us": [round(o, 2) for o in offs[-5:]],
-           "start_offset_mean_us": round(st.mean(offs), 2),
+           "start_offset_mean_us": round(st.mean(offs), 2), "streams": streams,
            "per_step": steps}
     print(json.dumps({k: v for k, v in res.items() if k != "per_step"}, indent=1))
     if a.out:

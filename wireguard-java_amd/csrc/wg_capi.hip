@@ -121,6 +121,9 @@ struct wg_ctx {
   // mixed-length WG_F_AFTER_SEAL steps through k_step_claim (dynamic claims over the longest-first
   // order) instead of the static snake (WG_CLAIM=1; A/B)
   bool claim = false;
+  // WG_F_AFTER_SEAL steps with the stitched Horner (transport_body ST: a round's Horner steps interleaved
+  // into the next round's ChaCha20 rounds; WG_STITCH=0|1, A/B)
+  bool stitch = false;
   // test hook WG_TEST_STEP_FLIP=N (power of two): the k_step launch's seal half writes a wrong tag for every
   // packet whose index is a multiple of N (tests/test_gpu_bench.py: the bench must report verified false)
   uint32_t test_flip = 0;
@@ -674,16 +677,28 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
       hipEvent_t ev;
       record_start(c, s, &ev);
       if (claim_nc) hipLaunchKernelGGL((wgt::k_step_claim<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+      else if (PS.n_long && sp.gs == 4 && c->stitch)
+        hipLaunchKernelGGL((wgt::k_step_mixed<4, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else if (PS.n_long && sp.gs == 4) hipLaunchKernelGGL(wgt::k_step_mixed<4>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+      else if (PS.n_long && c->stitch)
+        hipLaunchKernelGGL((wgt::k_step_mixed<8, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else if (PS.n_long) hipLaunchKernelGGL(wgt::k_step_mixed<8>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
 #ifdef WG_TEST_HOOKS
       else if (c->test_flip && G == 8)  // test hook build: the same body with the tag flip between the halves
         hipLaunchKernelGGL((wgt::k_step<8, 4, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, c->test_flip);
 #endif
+      else if (G == 16 && c->stitch)
+        hipLaunchKernelGGL((wgt::k_step<16, WG_STITCH_WPE, false, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
       else if (G == 16) hipLaunchKernelGGL(wgt::k_step<16>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
+      else if (G == 4 && c->stitch)
+        hipLaunchKernelGGL((wgt::k_step<4, WG_STITCH_WPE, false, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
       else if (G == 4) hipLaunchKernelGGL(wgt::k_step<4>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
+      else if (c->step_wpe4 && 2ull * gs * wgt::TW <= cap && c->stitch)
+        hipLaunchKernelGGL((wgt::k_step<8, WG_STITCH_WPE, false, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
       else if (c->step_wpe4 && 2ull * gs * wgt::TW <= cap)
         hipLaunchKernelGGL((wgt::k_step<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
+      else if (c->stitch)
+        hipLaunchKernelGGL((wgt::k_step<8, WG_STITCH_WPE, false, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
       else hipLaunchKernelGGL(wgt::k_step<8>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
       const hipError_t e = hipGetLastError();
       record_end(c, s, ev);
@@ -801,6 +816,7 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   if (const char* e = getenv("WG_PRIO")) c->prio_mode = atoi(e);
   if (const char* e = getenv("WG_STEP_WPE4")) c->step_wpe4 = atoi(e) != 0;
   if (const char* e = getenv("WG_CLAIM")) c->claim = atoi(e) != 0;
+  if (const char* e = getenv("WG_STITCH")) c->stitch = atoi(e) != 0;
 #ifdef WG_TEST_HOOKS
   // fault-injection hooks exist only in the test library (make test: libwgaead_test.so); the product
   // library never reads these variables, so no environment can make it write wrong tags

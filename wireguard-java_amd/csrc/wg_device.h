@@ -253,8 +253,55 @@ __device__ __forceinline__ void poly_mul(uint32_t h[5], const uint32_t r[5], con
 // previous limb's carry instead of the compiler adding the carry to a separately formed
 // chain: -1.4% VALU instructions per k_transport launch (SQ_INSTS_VALU 37.70 M -> 37.18 M on
 // C1), bit-exact. ASM = false: the same chains with compiler-visible products (mad64c).
+// One limb's five products as ONE asm statement: d = a0 b0 + a1 b1 + ... + a4 b4 + c, a chain of dependent
+// v_mad_u64_u32 with no pads inside (the compiler pads only at an asm statement's boundary, so five chains
+// per product cost 5 s_nop 0 instead of the 25 of one asm statement per v_mad_u64_u32).
+__device__ __forceinline__ uint64_t mad5(uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1, uint32_t a2, uint32_t b2,
+                                         uint32_t a3, uint32_t b3, uint32_t a4, uint32_t b4, uint64_t c) {
+  uint64_t d, cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %12\n\t"
+      "v_mad_u64_u32 %0, %1, %4, %5, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %6, %7, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %8, %9, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %10, %11, %0"
+      : "=&v"(d), "=&s"(cc)
+      : "v"(a0), "v"(b0), "v"(a1), "v"(b1), "v"(a2), "v"(b2), "v"(a3), "v"(b3), "v"(a4), "v"(b4), "v"(c));
+  return d;
+}
+__device__ __forceinline__ uint64_t mad5z(uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1, uint32_t a2, uint32_t b2,
+                                          uint32_t a3, uint32_t b3, uint32_t a4, uint32_t b4) {  // mad5 with c = 0
+  uint64_t d, cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, 0\n\t"
+      "v_mad_u64_u32 %0, %1, %4, %5, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %6, %7, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %8, %9, %0\n\t"
+      "v_mad_u64_u32 %0, %1, %10, %11, %0"
+      : "=&v"(d), "=&s"(cc)
+      : "v"(a0), "v"(b0), "v"(a1), "v"(b1), "v"(a2), "v"(b2), "v"(a3), "v"(b3), "v"(a4), "v"(b4));
+  return d;
+}
 template <bool ASM = true>
 __device__ __forceinline__ void poly_mul(uint32_t h[5], const uint32_t r[5], const uint32_t s[5]) {
+#ifdef WG_POLY_CHAIN5
+  if constexpr (ASM) {
+    const uint32_t h0 = h[0], h1 = h[1], h2 = h[2], h3 = h[3], h4 = h[4];
+    uint64_t d = mad5z(h4, s[1], h3, s[2], h2, s[3], h1, s[4], h0, r[0]);
+    h[0] = (uint32_t)d & M26;
+    d = mad5(h0, r[1], h1, r[0], h2, s[4], h3, s[3], h4, s[2], d >> 26);
+    h[1] = (uint32_t)d & M26;
+    d = mad5(h0, r[2], h1, r[1], h2, r[0], h3, s[4], h4, s[3], d >> 26);
+    h[2] = (uint32_t)d & M26;
+    d = mad5(h0, r[3], h1, r[2], h2, r[1], h3, r[0], h4, s[4], d >> 26);
+    h[3] = (uint32_t)d & M26;
+    d = mad5(h0, r[4], h1, r[3], h2, r[2], h3, r[1], h4, r[0], d >> 26);
+    h[4] = (uint32_t)d & M26;
+    uint32_t c = (uint32_t)(d >> 26);
+    h[0] += c * 5u;
+    c = h[0] >> 26; h[0] &= M26;
+    h[1] += c;
+    return;
+  }
+#endif
   auto mad = [](uint32_t a, uint32_t b, uint64_t c) { return ASM ? mad64(a, b, c) : mad64c(a, b, c); };
   const uint32_t h0 = h[0], h1 = h[1], h2 = h[2], h3 = h[3], h4 = h[4];
   uint64_t d = mad(h0, r[0], mad(h1, s[4], mad(h2, s[3], mad(h3, s[2], (uint64_t)h4 * s[1]))));

@@ -49,6 +49,7 @@
 
 #include "wg_device.h"
 #include "wg_kernels.h"
+#include "wg_stitch.h"
 
 namespace wgt {
 
@@ -340,12 +341,17 @@ __device__ __forceinline__ uint32_t opaque_lane() {
 // kPosChain, the positions a kPosClaim seal half logged, in the same order.
 constexpr int kPosStatic = 0, kPosClaim = 1, kPosChain = 2;
 
-template <int MODE, int G = 8, bool VF = false, int PM = kPosStatic>
+// ST (stitched Horner): a round's Horner steps run in the NEXT round of the packet, interleaved
+// into the first kStitchDR double rounds of its ChaCha20 block (wg_stitch.h); the next round's payload DMA is
+// issued after them, so the image still holds the round's MAC input while they read it. A packet's last
+// round takes its Horner steps after its XOR phase as before (nothing follows it to hide them in).
+template <int MODE, int G = 8, bool VF = false, int PM = kPosStatic, bool ST = false>
 __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_t blk, uint32_t wv, uint4* const img,
                                                SlotRec* const rec, uint32_t& iter) {
   static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
   static_assert(G == 4 || G == 8 || G == 16, "slots of 4, 8 or 16 lanes");
   static_assert(!VF || MODE == WG_MODE_OPEN, "verify-first is an open variant");
+  static_assert(!(ST && VF), "the verify-first open keeps the sequential Horner");
   constexpr uint32_t SH = G == 4 ? 2u : G == 8 ? 3u : 4u;  // log2 G
   constexpr uint32_t JM = G - 1u;
   if (P.prio_step && iter == 0) __builtin_amdgcn_s_setprio(3);  // first instruction: a fresh wave is never starved
@@ -510,12 +516,16 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
     const uint4 meta = rec[opaque_lane() >> SH].meta;
     const uint32_t len = meta.z;
     const uint32_t nb = (meta.w & 1u) ? ((len + 63u) >> 6) + 1u : 0u;
+    // ST: slots whose previous round (not their packet's last) still owes its Horner steps
+    const bool pend = ST && have && round > 0u && (meta.w & 1u);
+    const bool stitch = ST && __any(pend);
     uint32_t x[16];
     {
       // ---- payload prefetch: LDS-DMA straight into this lane's slice of the image ---------
-      // (no registers held across the ARX rounds)
+      // (no registers held across the ARX rounds; with stitched Horner steps pending, after them)
       const uint32_t lane = opaque_lane(), s = lane >> SH, j = lane & JM;
       const uint32_t b = G * round + j;
+      auto payload_dma = [&]() {
       if (have && b < nb && b > 0u) {
         const uint32_t off = 64u * (b - 1u);
         const uint32_t nbytes = min(64u, len - off);
@@ -534,6 +544,8 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
             if (16u * q < nbytes) img[64u * q + lane] = chunk_any(src + 16u * q, min(16u, nbytes - 16u * q));
         }
       }
+      };
+      if (!stitch) payload_dma();
       // ---- ChaCha20: block b = 8 round + j ----------------------------------------------
       if (__any(have && round == 0)) {  // a new packet: its columns 1..3 of the first round, once
         const uint32_t c = j & 3u;
@@ -552,7 +564,44 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         const uint32_t H[12] = {bcastg<G, 1>(hc[0]), bcastg<G, 1>(hc[1]), bcastg<G, 1>(hc[2]), bcastg<G, 1>(hc[3]),
                                 bcastg<G, 2>(hc[0]), bcastg<G, 2>(hc[1]), bcastg<G, 2>(hc[2]), bcastg<G, 2>(hc[3]),
                                 bcastg<G, 3>(hc[0]), bcastg<G, 3>(hc[1]), bcastg<G, 3>(hc[2]), bcastg<G, 3>(hc[3])};
-        chacha20_block_hoisted(rec[s].key, b, meta.x, meta.y, 0u, H, x);
+        if constexpr (!ST) {
+          chacha20_block_hoisted(rec[s].key, b, meta.x, meta.y, 0u, H, x);
+        } else {
+          // the same block in two parts: the first kStitchDR double rounds (with the pending Horner steps of the
+          // previous round when any slot has them), then the payload DMA, then the rest and the feed-forward
+          const uint4* kl = rec[s].key;
+          uint4 ka = kl[0], kb = kl[1];
+          x[0] = 0x61707865u; x[1] = H[0]; x[2] = H[4]; x[3] = H[8];
+          x[4] = ka.x; x[5] = H[1]; x[6] = H[5]; x[7] = H[9];
+          x[8] = kb.x; x[9] = H[2]; x[10] = H[6]; x[11] = H[10];
+          x[12] = b; x[13] = H[3]; x[14] = H[7]; x[15] = H[11];
+          if (stitch) {
+            // the previous round kp's window: chunks [4 G kp - 4, 4 G kp + 4 G - 4) (round 0's first four are the
+            // zeroed key-block lane, so every lane takes exactly four steps); lane j's chunks c0 + G t sit in one
+            // image row (c0 & 3), G / 4 lanes apart. Lanes without a pending round compute on a clamped address
+            // and their accumulator is not used (a new packet resets it in its round 0 scan).
+            const uint32_t kp = round - 1u;
+            const uint32_t nc = (len + 15u) >> 4, M = nc + 1u, Dp = G * ((M + JM) >> SH) - M;
+            const uint32_t u = 4u * G * kp + ((j - ((4u * G * kp - 4u + Dp) & JM)) & JM);  // c0 + 4
+            const uint32_t lanepart = ((u >> 2) - G * kp) & (G / 4u - 1u);
+            const uint32_t addr = (uint32_t)(uintptr_t)&img[64u * (u & 3u) + (lane & ~JM) + lanepart];
+            const uint4 q0 = rec[s].R0, q1 = rec[s].R1, q2 = rec[s].R2;
+            const uint32_t R[5] = {q0.x, q0.y, q0.z, q0.w, q1.x};
+            const uint32_t Rs[4] = {q1.y, q1.z, q1.w, q2.x};
+            chacha20_rounds_stitch_asm<G>(x, acc, R, Rs, addr);
+            payload_dma();
+          } else {
+            chacha20_rounds_head_asm(x);
+          }
+          chacha20_rounds_tail_asm(x);
+          asm volatile("" ::: "memory");
+          ka = kl[0];
+          kb = kl[1];
+          x[0] += 0x61707865u; x[1] += 0x3320646eu; x[2] += 0x79622d32u; x[3] += 0x6b206574u;
+          x[4] += ka.x; x[5] += ka.y; x[6] += ka.z; x[7] += ka.w;
+          x[8] += kb.x; x[9] += kb.y; x[10] += kb.z; x[11] += kb.w;
+          x[12] += b; x[13] += meta.x; x[14] += meta.y;
+        }
       }
     }
 
@@ -598,6 +647,11 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
               store_chunk(dst + 16u * q, cb, o, oal);
           }
         }
+      }
+      // ST: the key-block lane's image slice is round 0's chunks -4..-1 of the stitched window: zero
+      if (ST && have && round == 0u && j == 0u) {
+#pragma unroll
+        for (uint32_t q = 0; q < 4u; ++q) img[64u * q + lane] = make_uint4(0u, 0u, 0u, 0u);
       }
     }
     // the length block le64(0) || le64(len) is MAC chunk nc (the first after the data): the lane
@@ -656,8 +710,8 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
     }
 
     WG_PH(3);
-    // ---- Poly1305 over this round's chunks -------------------------------------------------
-    if (have && (meta.w & 1u) && mac_pass) {
+    // ---- Poly1305 over this round's chunks (ST: only a packet's last round; the others run stitched) -------
+    if (have && (meta.w & 1u) && mac_pass && (!ST || G * (round + 1u) >= nb)) {
       const uint32_t lane = opaque_lane(), s = lane >> SH, j = lane & JM;
       {
         const uint32_t nc = (len + 15u) >> 4;
@@ -872,8 +926,11 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
   else if (g == GS) transport_body<MODE, GS, VF>(Q, qb, wv, img_[wv], rec_[wv], iter);
 }
 
-template <int GS = 8>
-__global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)))
+#ifndef WG_STITCH_WPE
+#define WG_STITCH_WPE 5  // waves per SIMD the stitched kernels' register allocation targets (96 VGPRs: no spill)
+#endif
+template <int GS = 8, bool ST = false>
+__global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(ST ? WG_STITCH_WPE : 8)))
 k_step_mixed(TransportParams S, TransportParams O) {
   __shared__ uint4 img_[TW][4 * 64];
   __shared__ SlotRec rec_[TW][64 / GS];
@@ -883,13 +940,13 @@ k_step_mixed(TransportParams S, TransportParams O) {
   const int g = mixed_part<GS>(S, blockIdx.x, QS, qb);
   (void)mixed_part<GS>(O, blockIdx.x, QO, qb2);  // the same split: the open batch has the seal's lengths
   if (g == 16) {
-    transport_body<WG_MODE_SEAL, 16>(QS, qb, wv, img_[wv], rec_[wv], iter);
+    transport_body<WG_MODE_SEAL, 16, false, kPosStatic, ST>(QS, qb, wv, img_[wv], rec_[wv], iter);
     asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
-    transport_body<WG_MODE_OPEN, 16>(QO, qb, wv, img_[wv], rec_[wv], iter);
+    transport_body<WG_MODE_OPEN, 16, false, kPosStatic, ST>(QO, qb, wv, img_[wv], rec_[wv], iter);
   } else if (g == GS) {
-    transport_body<WG_MODE_SEAL, GS>(QS, qb, wv, img_[wv], rec_[wv], iter);
+    transport_body<WG_MODE_SEAL, GS, false, kPosStatic, ST>(QS, qb, wv, img_[wv], rec_[wv], iter);
     asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
-    transport_body<WG_MODE_OPEN, GS>(QO, qb, wv, img_[wv], rec_[wv], iter);
+    transport_body<WG_MODE_OPEN, GS, false, kPosStatic, ST>(QO, qb, wv, img_[wv], rec_[wv], iter);
   }
 }
 
@@ -950,19 +1007,19 @@ __device__ __forceinline__ void step_test_flip(const TransportParams& S, uint32_
 
 // FLIP: the test-hook instantiation (WG_TEST_STEP_FLIP), launched only by the test library (WG_TEST_HOOKS);
 // the product instantiations carry no hook code at all.
-template <int G = 8, int WPE = 8, bool FLIP = false>
+template <int G = 8, int WPE = 8, bool FLIP = false, bool ST = false>
 __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_step(TransportParams S, TransportParams O, uint32_t test_flip) {
   __shared__ uint4 img_[TW][4 * 64];
   __shared__ SlotRec rec_[TW][64 / G < 8 ? 8 : 64 / G];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t iter = 0;  // one issue-priority schedule over both halves (plan_transport: prio_step of the step)
-  transport_body<WG_MODE_SEAL, G>(S, blockIdx.x, wv, img_[wv], rec_[wv], iter);
+  transport_body<WG_MODE_SEAL, G, false, kPosStatic, ST>(S, blockIdx.x, wv, img_[wv], rec_[wv], iter);
   // the open reads the ciphertext and tags this wave just stored: wait until the stores are
   // performed and drop this CU's L1 lines (an in-place seal read the plaintext through them)
   asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
   if constexpr (FLIP) step_test_flip<G>(S, blockIdx.x, wv, test_flip);
-  transport_body<WG_MODE_OPEN, G>(O, blockIdx.x, wv, img_[wv], rec_[wv], iter);
+  transport_body<WG_MODE_OPEN, G, false, kPosStatic, ST>(O, blockIdx.x, wv, img_[wv], rec_[wv], iter);
 }
 
 // k_step with dynamic claims (mixed-length batches, WG_CLAIM): the seal half claims its slots' packets

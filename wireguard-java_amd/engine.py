@@ -154,6 +154,31 @@ class Engine:
         L.check(self._lib.wg_duplex_batch(self.ctx, ctypes.byref(sb), ctypes.byref(ob),
                                           stream if stream is not None else _torch_stream()))
 
+    def prepare_duplex(self, seal_desc, seal_in, seal_out, seal_max_len: int, open_desc, open_in, open_out, status,
+                       open_max_len: int, uniform: bool = False, after_seal: bool = False, stream: int | None = None):
+        """The same wg_duplex_batch call as duplex(), with its argument structs built once: returns a
+        zero-argument callable that issues the launch on `stream` (default: torch's current stream when
+        prepared). A caller that re-launches one batch layout over and over (a pipeline stage, a bench
+        step) so pays one foreign call per launch instead of rebuilding the arguments. The tensors must
+        stay alive and in place while the callable is used."""
+        u = L.WG_F_UNIFORM if uniform else 0
+        sb = L.WgBatch(seal_desc.data_ptr(), seal_in.data_ptr(), seal_out.data_ptr(), None, seal_in.numel(),
+                       seal_out.numel(), seal_desc.shape[0], seal_max_len, u, 0)
+        ob = L.WgBatch(open_desc.data_ptr(), open_in.data_ptr(), open_out.data_ptr(),
+                       status.data_ptr() if status is not None else None, open_in.numel(), open_out.numel(),
+                       open_desc.shape[0], open_max_len, u | (L.WG_F_AFTER_SEAL if after_seal else 0), 0)
+        fn, ctx = self._lib.wg_duplex_batch, self.ctx
+        ps, po = ctypes.byref(sb), ctypes.byref(ob)
+        st = stream if stream is not None else _torch_stream()
+        keep = (sb, ob, seal_desc, seal_in, seal_out, open_desc, open_in, open_out, status)
+
+        def launch():
+            rc = fn(ctx, ps, po, st)
+            if rc < 0:
+                L.check(rc)
+            return keep  # (holds the structs and tensors for as long as the callable lives)
+        return launch
+
     # ---- receive side after open (wg_rx_check) -------------------------------------
     def filter_set(self, filter_id: int, prefixes) -> None:
         """wg_filter_set from (address string or ipaddress object, prefix_len) pairs, as
