@@ -503,8 +503,9 @@ def main():
             # m packets starting at a quarter of the half wrap around it and stay contiguous
             m = n - cuts[1]
             q = m // 2
-            desc2 = torch.cat([d_desc[cuts[1]:], d_desc[cuts[1]:]])
-            st2 = torch.zeros(2 * m, dtype=torch.int32, device=dev)
+            desc2 = torch.cat([d_desc[cuts[1]:], d_desc[cuts[1]:cuts[1] + q]])  # B's half, then its first quarter again
+            st2 = torch.zeros(m + q, dtype=torch.int32, device=dev)
+            st2_used = m + q if args.steps >= 2 else m  # a one-step window runs Q1 and Q2 only
             sb = side[1].cuda_stream
             prep_q1 = eng.prepare_duplex(desc2[:q], pt, ct, max_len, desc2[:q], ct, back, st2[:q], max_len,
                                          uniform=uniform, after_seal=True, stream=sb)
@@ -659,7 +660,7 @@ def main():
     # oracle. The re-timing and the per-kernel trains after this overwrite ct / back / status.
     window_launches = launch_count[0] - launches_before
     if st2 is not None:  # stream B's packets report through its ring of statuses
-        ok_status = int(status[:cuts[1]].abs().sum().item()) == 0 and int(st2.abs().sum().item()) == 0
+        ok_status = int(status[:cuts[1]].abs().sum().item()) == 0 and int(st2[:st2_used].abs().sum().item()) == 0
     else:
         ok_status = int(status.abs().sum().item()) == 0
     if uniform:  # equal strides: compare the [n, L] payload views directly

@@ -67,10 +67,10 @@ def test_bench_two_stream_step_every_packet_vs_oracle(engine):
     assert np.array_equal(back[:, :L], pt.reshape(n, stride)[:, :L])
 
 
-def _bench(extra_env):
+def _bench(extra_env, steps="2", *extra):
     env = dict(os.environ, **extra_env)
-    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
-                        "--ramp-ms", "0"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", steps, "--warmup", "1",
+                        "--ramp-ms", "0", *extra], cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert lines, f"no JSON line (rc {p.returncode}): {p.stderr[-2000:]}"
     return p.returncode, json.loads(lines[-1])
@@ -92,5 +92,13 @@ def test_bench_line_fails_when_k_step_writes_a_wrong_tag():
     assert rc == 0, line
     assert line["verified"] is True and line["oracle_sample"]["bit_exact"] is True
     assert line["config"]["streams"] == 2 and line["roofline"]["kernel_names"] == ["k_step"]
+    # the staggered two-stream schedule: 2 steps = 2 launches on stream A, Q1 + 1 window + Q2 on stream B
+    assert line["stagger"] is True and line["window_launches"] == 5
+    for steps in ("1", "3"):
+        rc, line = _bench({}, steps)
+        assert rc == 0 and line["verified"] is True and line["oracle_sample"]["bit_exact"] is True, line
+        assert line["window_launches"] == 2 * int(steps) + 1
+    rc, line = _bench({}, "2", "--stagger", "0")
+    assert rc == 0 and line["verified"] is True and line["stagger"] is False and line["window_launches"] == 4
     rc, line = _bench({"WG_TEST_STEP_FLIP": "64"})  # the product library: no hook, still bit-exact
     assert rc == 0 and line["verified"] is True and line["oracle_sample"]["bit_exact"] is True

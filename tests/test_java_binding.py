@@ -39,3 +39,12 @@ def test_every_java_downcall_matches_the_header():
         args = kinds[1:]  # first is the return layout
         want = [_c_kind(a) for a in protos[name]]
         assert args == want, (name, args, want)
+
+
+def test_java_no_key_code_matches_the_header():
+    """WgAead.check turns WG_ENOKEY (a cleaned or never-set key slot) into IllegalStateException, as the
+    reference's closed key arena does; the constant must be the header's."""
+    c = int(re.search(r"#define WG_ENOKEY \((-\d+)\)", HDR).group(1))
+    j = int(re.search(r"static final int WG_ENOKEY = (-\d+);", JAVA).group(1))
+    assert c == j
+    assert "throw new IllegalStateException" in JAVA

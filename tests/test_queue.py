@@ -226,7 +226,7 @@ def test_queued_packets_keep_the_key_they_were_submitted_with():
             assert data == O.c_aead_seal(key, O.transport_nonce(i), pts[i]), i
         # every completed batch's key copies are wiped from the pinned ring (they stayed until
         # the queue was freed, so a zeroed session's key outlived clean() in pinned memory)
-        assert W._lib.wg_queue_key_residue(q.q) == 0
+        assert W.lib().wg_queue_key_residue(q.q) == 0
     finally:
         if q is not None:
             q.close()
@@ -500,7 +500,7 @@ def test_no_key_left_in_the_ring_after_reap():
             assert len(got) == 200
             if mode == "seal":
                 assert all(st == 0 for _, st, _ in got.values())
-            assert W._lib.wg_queue_key_residue(q.q) == 0
+            assert W.lib().wg_queue_key_residue(q.q) == 0
             with pytest.raises(W.WgError) as ei:
                 q.submit(2, 0, b"x" * (8 + extra), 0)  # never set
             assert ei.value.code == W._lib.WG_ENOKEY

@@ -160,18 +160,22 @@ def test_stitched_asm_matches_rounds_and_horner(G):
         ops["%30"] = 0
         ops.update({f"%{31 + i}": R[i] for i in range(5)})
         ops.update({f"%{36 + i}": 5 * R[i + 1] & M32 for i in range(4)})
-        ops["%40"], ops["%41"], ops["%42"] = base, M26, 1 << 24
+        virt = trial % 3 == 2  # a lane whose step 0 is a virtual chunk before a packet's data: no 2^128 bit
+        ops["%40"], ops["%41"], ops["%42"], ops["%43"] = base, M26, 1 << 24, 0 if virt else 1 << 24
         regs = emulate(lines, ops, lds)
         assert [regs[f"%{i}"] for i in range(16)] == chacha_half(x, ndr)
         h = list(acc)
         for t in range(4):
             h = poly_mul(h, R)
-            h = [a + b for a, b in zip(h, chunk_limbs(chunks[t]))]
+            m = chunk_limbs(chunks[t])
+            if virt and t == 0:
+                m[4] -= 1 << 24
+            h = [a + b for a, b in zip(h, m)]
         got = [regs[f"%{16 + i}"] for i in range(5)]
         assert got == h, (G, trial)
         want = val(acc)
         for t in range(4):
-            want = (want * val(R) + val(chunk_limbs(chunks[t]))) % P
+            want = (want * val(R) + val(chunk_limbs(chunks[t])) - ((1 << 128) if virt and t == 0 else 0)) % P
         assert val(got) % P == want
 
 

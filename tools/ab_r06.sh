@@ -13,8 +13,8 @@ cd $ROOT
 die() { echo "[ab] FAILED: $1 (rc $2)"; exit $2; }
 PYT="python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu"
 if [ "$PART" != ab ]; then
-  echo "[ab] GPU suite (product library)"
-  timeout -k 10 900 $PYT tests > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; die tests $?; }
+  echo "[ab] GPU suite (product library), the bench tests first"
+  timeout -k 10 900 $PYT tests/test_gpu_bench.py tests > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; die tests $?; }
   tail -1 $O/gpu_tests.log
   echo "[ab] stitched kernels through the configuration and step tests"
   WG_STITCH=1 timeout -k 10 600 $PYT tests/test_gpu_configs.py tests/test_gpu_duplex.py tests/test_gpu_bench.py > $O/st_tests.log 2>&1 || { tail -30 $O/st_tests.log; die st_tests $?; }

@@ -19,6 +19,8 @@ Layout of the statement (operands):
   %40       the LDS byte address of the lane's first chunk of the window
   %41       sgpr: 0x3ffffff
   %42       sgpr: 1 << 24 (the chunk's 2^128 bit in limb 4)
+  %43       vgpr: the 2^128 bit of step 0's chunk (0 for a lane whose first step of a packet's round 0 is a
+            virtual chunk before the data: it reads the zeroed key-block lane, and without the bit it adds 0)
   v[62:63]  the 64-bit accumulator of one limb's product chain (clobbered: a register pair's halves
             cannot be named through an asm operand)
 Every instruction is an 8-byte encoding (VOP3 / DS), so the placed stream keeps the ChaCha20 rounds'
@@ -38,7 +40,7 @@ W = [f"%{26 + i}" for i in range(4)]
 CC = "%30"
 R = [f"%{31 + i}" for i in range(5)]
 S = [None] + [f"%{36 + i}" for i in range(4)]
-ADDR, M26, HIB = "%40", "%41", "%42"
+ADDR, M26, HIB, HIB0 = "%40", "%41", "%42", "%43"
 D, DLO, DHI = "v[62:63]", "v62", "v63"
 
 
@@ -112,7 +114,7 @@ def horner_step(t, G, H, N, last):
         out.append(f"v_and_b32_e64 {DLO}, {DLO}, {M26}")
         out.append(f"v_add_u32_e64 {N[k]}, {N[k]}, {DLO}")
     out.append(f"v_lshrrev_b32_e64 {DLO}, 8, {W[3]}")
-    out.append(f"v_add3_u32 {N[4]}, {N[4]}, {DLO}, {HIB}")
+    out.append(f"v_add3_u32 {N[4]}, {N[4]}, {DLO}, {HIB0 if t == 0 else HIB}")
     if not last:
         out += loads(t + 1, G)
     return out
@@ -172,7 +174,7 @@ namespace wgd {
 
 constexpr int kStitchDR = {NDR};  // double rounds in the stitched first part (the rest: chacha20_rounds_tail_asm)
 
-#define WG_STITCH_OPS(x, h, n, r, s, w, addr, m26, cc, hib)                                                \\
+#define WG_STITCH_OPS(x, h, n, r, s, w, addr, m26, cc, hib, hib0)                                          \\
   : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),       \\
     "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]), "+v"(x[15]), \\
     "+v"(h[0]), "+v"(h[1]), "+v"(h[2]), "+v"(h[3]), "+v"(h[4]),                                           \\
@@ -180,7 +182,7 @@ constexpr int kStitchDR = {NDR};  // double rounds in the stitched first part (t
     "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&s"(cc)                                         \\
   : "v"(r[0]), "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]),                                                \\
     "v"(s[0]), "v"(s[1]), "v"(s[2]), "v"(s[3]),                                                           \\
-    "v"(addr), "s"(m26), "s"(hib)                                                                         \\
+    "v"(addr), "s"(m26), "s"(hib), "v"(hib0)                                                              \\
   : "v62", "v63", "memory"
 '''
 
@@ -189,14 +191,14 @@ FUNC = '''
 // acc = ((((acc R + m0) R + m1) R + m2) R + m3), m_t the 16-B chunk at LDS byte address addr + {STEP} t.
 template <>
 __device__ __forceinline__ void chacha20_rounds_stitch_asm<{G}>(uint32_t x[16], uint32_t acc[5], const uint32_t R[5],
-                                                                const uint32_t Rs[4], uint32_t addr) {
+                                                                const uint32_t Rs[4], uint32_t addr, uint32_t hib0) {
   uint32_t n[5], w[4];
   const uint32_t m26 = 0x3ffffffu, hib = 1u << 24;
   uint64_t cc;
   asm volatile(
     ".p2align 3\\n\\ts_nop 0\\n\\t"
     "{BODY}\\n"
-    WG_STITCH_OPS(x, acc, n, R, Rs, w, addr, m26, cc, hib));
+    WG_STITCH_OPS(x, acc, n, R, Rs, w, addr, m26, cc, hib, hib0));
   (void)n; (void)w; (void)cc;
 }
 '''
@@ -222,7 +224,7 @@ def main():
     s += '''
 template <int G>
 __device__ __forceinline__ void chacha20_rounds_stitch_asm(uint32_t x[16], uint32_t acc[5], const uint32_t R[5],
-                                                           const uint32_t Rs[4], uint32_t addr);
+                                                           const uint32_t Rs[4], uint32_t addr, uint32_t hib0);
 '''
     for G in (4, 8, 16):
         body = emit(gen(G, ndr))

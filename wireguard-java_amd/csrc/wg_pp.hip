@@ -399,13 +399,13 @@ __device__ void pp_serve(Unit& U, const PPParams& P, uint32_t i, uint64_t t_seen
     if (P.svc) {
       __hip_atomic_store(P.svc + i, __builtin_amdgcn_s_memrealtime() - t_seen, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
-      // two relaxed stores to different addresses are not ordered by the memory model: the completion
-      // word is stored with release semantics below, so a caller that sees it also sees this value
+      // two relaxed stores to different addresses are not ordered by the memory model: the completion word
+      // is issued only once this store has been performed (both are system-scope write-through stores), so a
+      // caller that sees the completion also sees this value. (A release store here would also write back the
+      // whole L2 before the completion: 2.9-ms calls in r06b.)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    if (P.svc)
-      __hip_atomic_store(P.done + i, (seq << 8) | status, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    else
-      __hip_atomic_store(P.done + i, (seq << 8) | status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(P.done + i, (seq << 8) | status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

@@ -588,7 +588,10 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
             const uint4 q0 = rec[s].R0, q1 = rec[s].R1, q2 = rec[s].R2;
             const uint32_t R[5] = {q0.x, q0.y, q0.z, q0.w, q1.x};
             const uint32_t Rs[4] = {q1.y, q1.z, q1.w, q2.x};
-            chacha20_rounds_stitch_asm<G>(x, acc, R, Rs, addr);
+            // a lane whose first chunk of round 0's window lies before the data (u < 4: chunks -4..-1) adds it
+            // without the 2^128 bit, so the zeroed chunk adds nothing to its still-zero accumulator
+            const uint32_t hib0 = (kp == 0u && u < 4u) ? 0u : (1u << 24);
+            chacha20_rounds_stitch_asm<G>(x, acc, R, Rs, addr, hib0);
             payload_dma();
           } else {
             chacha20_rounds_head_asm(x);

@@ -146,6 +146,9 @@ public final class WgAead {
 		return symbols.find(name).map(addr -> linker.downcallHandle(addr, fd)).orElseThrow();
 	}
 
+	/** include/wgaead.h WG_ENOKEY: a per-packet call or queue submit on a key slot without a key. */
+	static final int WG_ENOKEY = -126;
+
 	/** Negative return codes become RuntimeExceptions, as the reference's wrappers do (ChaCha20.java:102,110,141). */
 	static int check(int rc) {
 		if (rc < 0) {
@@ -159,6 +162,10 @@ public final class WgAead {
 			} catch (Throwable t) {
 				msg = "";
 			}
+			// WG_ENOKEY: the key slot was zeroed (clean()) or never set; the reference's cipher() / decipher()
+			// on a cleaned keypair fail on its closed key arena with an IllegalStateException
+			if (rc == WG_ENOKEY)
+				throw new IllegalStateException("libwgaead: key slot without a key (keypair cleaned): " + msg);
 			throw new RuntimeException("libwgaead error " + rc + ": " + msg);
 		}
 		return rc;
