@@ -45,6 +45,7 @@ for a in $(seq 1 $ALT); do
   for w in "--workload c1 --streams 1" "--workload c1" "--workload c2" "--workload imix"; do
     run base -- $w
     run st5 WG_STITCH=1 -- $w
+    [ "$w" = "--workload imix" ] && run base_lpt2 WG_LPT_ONE=0 -- $w
     for v in $(ls ab_libs 2>/dev/null); do
       run $v WG_LIB_PATH=$ROOT/ab_libs/$v/libwgaead.so WG_STITCH=$([ $v = st6 ] && echo 1 || echo 0) -- $w
     done

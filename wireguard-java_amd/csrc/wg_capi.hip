@@ -62,11 +62,17 @@ int fail(int code, const char* fmt, ...) {
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  // a histogram workspace used by k_lpt_one: its two counter sets (zeroed = both are zero or hold this
+  // buffer's counts), the set the next call counts into, the set the last call counted into
+  bool zeroed = false;
+  uint32_t par = 0;
+  uint32_t* last_cnt = nullptr;
   int ensure(size_t bytes) {
     if (bytes <= cap) return WG_OK;
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
+    zeroed = false;
     size_t want = std::max<size_t>(bytes, 256);
     if (hipMalloc(&p, want) != hipSuccess) return fail(WG_ENOMEM, "hipMalloc(%zu) failed", want);
     cap = want;
@@ -124,6 +130,8 @@ struct wg_ctx {
   // WG_F_AFTER_SEAL steps with the stitched Horner (transport_body ST: a round's Horner steps interleaved
   // into the next round's ChaCha20 rounds; WG_STITCH=0|1, A/B)
   bool stitch = false;
+  // the short-packet split plan's order in one launch (k_lpt_one; WG_LPT_ONE=0: k_lpt_hist + k_lpt_scatter)
+  bool lpt_one = true;
   // test hook WG_TEST_STEP_FLIP=N (power of two): the k_step launch's seal half writes a wrong tag for every
   // packet whose index is a multiple of N (tests/test_gpu_bench.py: the bench must report verified false)
   uint32_t test_flip = 0;
@@ -446,8 +454,30 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
   if (!(flags & WG_F_UNIFORM) && (per_slot > 1 || mixed || G == 4)) {
     // reuse_order: the order already in lpt_order (the seal of the same packets, WG_F_AFTER_SEAL);
     // private_ws: buffers owned by the caller's stream (no shared-workspace ordering)
-    if (!reuse_order) {
+    // one: the short-packet split plan orders in ONE launch (k_lpt_one: sparse order, double-buffered
+    // counters, no memset) instead of k_lpt_hist + k_lpt_scatter (WG_LPT_ONE=0: the two launches, A/B)
+    const bool one = mixed && max_len <= 2048u && !claim && c->lpt_one;
+    if (!reuse_order && one) {
       int rc;
+      if ((rc = lpt_hist.ensure(2 * 8 * sizeof(uint32_t))) != WG_OK) return rc;
+      if ((rc = lpt_order.ensure(sizeof(uint32_t) * wgt::kFastBins * (size_t)n)) != WG_OK) return rc;
+      if (!private_ws && (rc = ws_acquire(c, s)) != WG_OK) return rc;
+      if (!lpt_hist.zeroed) {  // a new buffer, or one the two-launch planner wrote histograms into
+        HIPTRY(hipMemsetAsync(lpt_hist.p, 0, 2 * 8 * sizeof(uint32_t), s));
+        lpt_hist.zeroed = true;
+        lpt_hist.par = 0;
+      }
+      uint32_t* cnt = (uint32_t*)lpt_hist.p + 8u * lpt_hist.par;
+      uint32_t* nxt = (uint32_t*)lpt_hist.p + 8u * (lpt_hist.par ^ 1u);
+      const uint32_t lgrid = std::max<uint32_t>(1u, std::min<uint32_t>(wgt::LPT_MAX_BLOCKS, (n + 1023u) / 1024u));
+      hipLaunchKernelGGL((wgt::k_lpt_one<MODE>), dim3(lgrid), dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len, cnt, nxt,
+                         (uint32_t*)lpt_order.p);
+      HIPTRY(hipGetLastError());
+      lpt_hist.last_cnt = cnt;
+      lpt_hist.par ^= 1u;
+    } else if (!reuse_order) {
+      int rc;
+      lpt_hist.zeroed = false;
       const uint32_t lgrid = std::max<uint32_t>(1u, std::min<uint32_t>(wgt::LPT_MAX_BLOCKS, (n + 1023u) / 1024u));
       if ((rc = lpt_hist.ensure(sizeof(uint32_t) * wgt::LPT_MAX_BLOCKS * wgt::LPT_BINS)) != WG_OK) return rc;
       if ((rc = lpt_order.ensure(sizeof(uint32_t) * (size_t)n)) != WG_OK) return rc;
@@ -461,7 +491,14 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
       HIPTRY(hipGetLastError());
     }
     P.order = (const uint32_t*)lpt_order.p;
-    if (mixed) P.n_long = (const uint32_t*)c->lpt_nlong.p;
+    if (one) {
+      P.bin_cnt = lpt_hist.last_cnt;
+      P.bin_cap = n;
+      P.split = split;
+      P.n_long = lpt_hist.last_cnt;  // (marks the launch as mixed)
+    } else if (mixed) {
+      P.n_long = (const uint32_t*)c->lpt_nlong.p;
+    }
     ordered = !private_ws;
   }
   *Pout = P;
@@ -817,6 +854,7 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   if (const char* e = getenv("WG_STEP_WPE4")) c->step_wpe4 = atoi(e) != 0;
   if (const char* e = getenv("WG_CLAIM")) c->claim = atoi(e) != 0;
   if (const char* e = getenv("WG_STITCH")) c->stitch = atoi(e) != 0;
+  if (const char* e = getenv("WG_LPT_ONE")) c->lpt_one = atoi(e) != 0;
 #ifdef WG_TEST_HOOKS
   // fault-injection hooks exist only in the test library (make test: libwgaead_test.so); the product
   // library never reads these variables, so no environment can make it write wrong tags

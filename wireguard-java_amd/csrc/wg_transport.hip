@@ -122,7 +122,16 @@ struct TransportParams {
   uint32_t prio_step;     // rounds per issue-priority level (0: no priority changes)
   const RxTables* rx;     // open with WG_F_RX_FILTER: receive-side verdict in the status (else NULL)
   const uint32_t* n_long; // k_*_mixed: device count of the packets at the front of the order that take
-                          // 16-lane slots (written by k_lpt_scatter); NULL otherwise
+                          // 16-lane slots (written by k_lpt_scatter); NULL otherwise. With bin_cnt (one-launch
+                          // planning, k_lpt_one) it only marks the launch as mixed.
+  // one-launch planning (k_lpt_one, batches of max_len <= 2048): the longest-first order is SPARSE, key k's
+  // packets at order[k * bin_cap ...], bin_cnt[k] of them; the kernel reads the counts into bc (mixed_part)
+  // and maps a batch position to its packet through them (pkt_at). pos_base: the position of this part's
+  // first packet in the whole order (the short part starts after the long one). split: keys > split are long.
+  const uint32_t* bin_cnt;
+  uint32_t bin_cap;
+  uint32_t pos_base;
+  uint32_t split;
   // dynamic claims (k_step_claim, mixed-length batches): the longest-first order is dealt
   // as claim_nc interleaved sub-orders (positions c, c + nc, c + 2 nc, ...), sub-order c to the workgroups
   // b with b % nc == c; each slot starts on a static position and claims every later one from its
@@ -303,6 +312,30 @@ __device__ __forceinline__ uint32_t batch_pos(uint32_t g, uint32_t k, uint32_t S
   return k * S + ((k & 1u) ? S - 1u - g : g);
 }
 
+#define WG_CONST __attribute__((address_space(4)))  // constant address space: scalar loads
+
+// batch position -> packet index: the identity, the dense longest-first order, or the sparse one of k_lpt_one
+// (keys descending, key k's packets at order[k * bin_cap + i])
+constexpr uint32_t kFastBins = 6;  // keys 0..5: every packet of at most 2,048 B (33 blocks, 5 rounds of 8)
+template <bool MX>
+__device__ __forceinline__ uint32_t pkt_at(const TransportParams& P, uint32_t pos) {
+  if (MX && P.bin_cap) {
+    // the counts through the scalar cache (constant for the launch), not held in SGPRs across the body
+    // (branch-free: the position's key region and its offset in it, one select per key)
+    const WG_CONST uint32_t* bc = (const WG_CONST uint32_t*)P.bin_cnt;
+    const uint32_t p = P.pos_base + pos;
+    uint32_t start = 0, at = 0;
+#pragma unroll
+    for (int k = (int)kFastBins - 1; k >= 0; --k) {
+      const uint32_t c = bc[k];
+      at = (p >= start) ? (uint32_t)k * P.bin_cap + (p - start) : at;
+      start += c;
+    }
+    return P.order[at];
+  }
+  return P.order ? P.order[pos] : pos;
+}
+
 // ---- the kernel ------------------------------------------------------------------------
 // Register budget: <= 64 VGPRs, so 8 waves share a SIMD (the payload stream and the ARX
 // rounds of other waves hide each other's latency). What is constant for a packet lives
@@ -321,7 +354,6 @@ struct SlotRec {  // per slot, in LDS
 };
 static_assert(sizeof(SlotRec) == 128, "slot record is 128 B");
 
-#define WG_CONST __attribute__((address_space(4)))  // constant address space: scalar loads
 
 __device__ __forceinline__ uint32_t opaque_lane() {
   uint32_t x = threadIdx.x & 63u;
@@ -345,7 +377,8 @@ constexpr int kPosStatic = 0, kPosClaim = 1, kPosChain = 2;
 // into the first kStitchDR double rounds of its ChaCha20 block (wg_stitch.h); the next round's payload DMA is
 // issued after them, so the image still holds the round's MAC input while they read it. A packet's last
 // round takes its Horner steps after its XOR phase as before (nothing follows it to hide them in).
-template <int MODE, int G = 8, bool VF = false, int PM = kPosStatic, bool ST = false>
+// MX: the launch is a k_*_mixed part (its positions may map through k_lpt_one's sparse order)
+template <int MODE, int G = 8, bool VF = false, int PM = kPosStatic, bool ST = false, bool MX = false>
 __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_t blk, uint32_t wv, uint4* const img,
                                                SlotRec* const rec, uint32_t& iter) {
   static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
@@ -381,7 +414,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
       pos = csub + P.claim_nc * gl;
     }
     npos = pos;
-    nxt = pos < P.n ? (P.order ? P.order[pos] : pos) : ~0u;
+    nxt = pos < P.n ? pkt_at<MX>(P, pos) : ~0u;
   }
   uint32_t dnext = 0u, dnext2 = 0u;
   if constexpr (G == 4) {
@@ -485,7 +518,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
       ++gen;
       if constexpr (PM == kPosStatic) {
         const uint32_t pos = batch_pos(g, gen, S);
-        nxt = pos < P.n ? (P.order ? P.order[pos] : pos) : ~0u;
+        nxt = pos < P.n ? pkt_at<MX>(P, pos) : ~0u;
       } else if constexpr (PM == kPosClaim) {
         cpos = npos;
         uint32_t k = 0;
@@ -898,9 +931,17 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
 // rest of the (host-sized, upper-bound) grid exits at once.
 template <int GS = 8>
 __device__ __forceinline__ int mixed_part(const TransportParams& P, uint32_t blk, TransportParams& Q, uint32_t& qblk) {
-  const uint32_t nl = min(__builtin_amdgcn_readfirstlane(*(const WG_CONST uint32_t*)P.n_long), P.n);
-  const uint32_t b16 = (nl + 4u * TW - 1u) / (4u * TW);
   Q = P;
+  uint32_t nl;
+  if (P.bin_cnt) {  // one-launch planning: the bins' counts, the long packets those of keys above the split
+    nl = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kFastBins; ++k) nl += k > P.split ? ((const WG_CONST uint32_t*)P.bin_cnt)[k] : 0u;
+    nl = min(nl, P.n);
+  } else {
+    nl = min(__builtin_amdgcn_readfirstlane(*(const WG_CONST uint32_t*)P.n_long), P.n);
+  }
+  const uint32_t b16 = (nl + 4u * TW - 1u) / (4u * TW);
   if (blk < b16) {
     Q.n = nl;
     Q.slots = b16 * TW * 4u;
@@ -910,7 +951,8 @@ __device__ __forceinline__ int mixed_part(const TransportParams& P, uint32_t blk
   constexpr uint32_t spw = 64u / GS;  // short slots per wave
   const uint32_t ns = P.n - nl, bs = (ns + spw * TW - 1u) / (spw * TW);
   if (blk - b16 >= bs) return 0;
-  Q.order = P.order + nl;
+  if (P.bin_cnt) Q.pos_base = nl;  // the sparse order's positions run on past the long packets
+  else Q.order = P.order + nl;
   Q.n = ns;
   Q.slots = bs * TW * spw;
   qblk = blk - b16;
@@ -925,8 +967,8 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
   TransportParams Q;
   uint32_t qb = 0, iter = 0;
   const int g = mixed_part<GS>(P, blockIdx.x, Q, qb);
-  if (g == 16) transport_body<MODE, 16, VF>(Q, qb, wv, img_[wv], rec_[wv], iter);
-  else if (g == GS) transport_body<MODE, GS, VF>(Q, qb, wv, img_[wv], rec_[wv], iter);
+  if (g == 16) transport_body<MODE, 16, VF, kPosStatic, false, true>(Q, qb, wv, img_[wv], rec_[wv], iter);
+  else if (g == GS) transport_body<MODE, GS, VF, kPosStatic, false, true>(Q, qb, wv, img_[wv], rec_[wv], iter);
 }
 
 #ifndef WG_STITCH_WPE
@@ -943,13 +985,13 @@ k_step_mixed(TransportParams S, TransportParams O) {
   const int g = mixed_part<GS>(S, blockIdx.x, QS, qb);
   (void)mixed_part<GS>(O, blockIdx.x, QO, qb2);  // the same split: the open batch has the seal's lengths
   if (g == 16) {
-    transport_body<WG_MODE_SEAL, 16, false, kPosStatic, ST>(QS, qb, wv, img_[wv], rec_[wv], iter);
+    transport_body<WG_MODE_SEAL, 16, false, kPosStatic, ST, true>(QS, qb, wv, img_[wv], rec_[wv], iter);
     asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
-    transport_body<WG_MODE_OPEN, 16, false, kPosStatic, ST>(QO, qb, wv, img_[wv], rec_[wv], iter);
+    transport_body<WG_MODE_OPEN, 16, false, kPosStatic, ST, true>(QO, qb, wv, img_[wv], rec_[wv], iter);
   } else if (g == GS) {
-    transport_body<WG_MODE_SEAL, GS, false, kPosStatic, ST>(QS, qb, wv, img_[wv], rec_[wv], iter);
+    transport_body<WG_MODE_SEAL, GS, false, kPosStatic, ST, true>(QS, qb, wv, img_[wv], rec_[wv], iter);
     asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
-    transport_body<WG_MODE_OPEN, GS, false, kPosStatic, ST>(QO, qb, wv, img_[wv], rec_[wv], iter);
+    transport_body<WG_MODE_OPEN, GS, false, kPosStatic, ST, true>(QO, qb, wv, img_[wv], rec_[wv], iter);
   }
 }
 
@@ -1138,6 +1180,31 @@ __global__ void __launch_bounds__(LPT_THREADS) k_lpt_scatter(const wg_pkt* d, ui
   __syncthreads();
   uint32_t lo, hi;
   lpt_range(n, lo, hi);
+  for (uint32_t i = lo + threadIdx.x; i < hi; i += LPT_THREADS) order[atomicAdd(&base[lpt_key<MODE>(d, i, max_len)], 1u)] = i;
+}
+
+// One launch instead of k_lpt_hist + k_lpt_scatter, for batches whose keys fit kFastBins (max_len <= 2,048 B,
+// the short-packet plan): each block counts its range's keys in LDS, takes its base in every non-empty key
+// with ONE atomicAdd on that key's global counter, and ranks its packets into the key's region of a sparse
+// order (key k at order[k * n]). No grid-wide barrier: the consumer derives the positions from the counts.
+// The counters are double-buffered by call (cnt for this call, zero on entry; cnt_next zeroed here for the
+// next), so no memset launch either. Order inside a key: arbitrary (every position of the order is a packet).
+template <int MODE>
+__global__ void __launch_bounds__(LPT_THREADS) k_lpt_one(const wg_pkt* d, uint32_t n, uint32_t max_len, uint32_t* cnt,
+                                                         uint32_t* cnt_next, uint32_t* order) {
+  __shared__ uint32_t h[kFastBins], base[kFastBins];
+  if (threadIdx.x < kFastBins) h[threadIdx.x] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < kFastBins) cnt_next[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t lo, hi;
+  lpt_range(n, lo, hi);
+  for (uint32_t i = lo + threadIdx.x; i < hi; i += LPT_THREADS) atomicAdd(&h[lpt_key<MODE>(d, i, max_len)], 1u);
+  __syncthreads();
+  if (threadIdx.x < kFastBins) {
+    const uint32_t k = threadIdx.x, c = h[k];
+    base[k] = k * n + (c ? atomicAdd(&cnt[k], c) : 0u);
+  }
+  __syncthreads();
   for (uint32_t i = lo + threadIdx.x; i < hi; i += LPT_THREADS) order[atomicAdd(&base[lpt_key<MODE>(d, i, max_len)], 1u)] = i;
 }
 
