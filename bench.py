@@ -398,7 +398,13 @@ def main():
     # window that wraps around its half, its last the remaining quarter), so the two streams' launches are half a
     # launch apart from the first step, as in a long run, and end together; every packet is still sealed and
     # opened exactly once per step. --stagger 0: both streams start and end on the same batch boundaries
-    ap.add_argument("--stagger", type=int, default=1, choices=[0, 1])
+    # (measured in round 6 on the driver's 20-step command, six alternations: medians 1,462 vs 1,470 GiB/s, the
+    # same GPU time per step; profiles/r06_stagger_ab.jsonl. Off by default: the plain batch-aligned schedule)
+    ap.add_argument("--stagger", type=int, default=0, choices=[0, 1])
+    # the end of the timed region is detected by polling the last event (as a pipeline stage polls its
+    # completion) instead of the blocking synchronize alone, whose wake-up adds to every run's wall time;
+    # --spin-sync 0: the blocking synchronize only
+    ap.add_argument("--spin-sync", type=int, default=1, choices=[0, 1])
     # duplex: each step is ONE wg_duplex_batch launch that seals this step's batch and opens
     # the previous step's ciphertext (double-buffered); serial: a seal launch, then an open
     # launch of the same batch
@@ -648,6 +654,9 @@ def main():
         join()  # ... and ev1 waits for all of them
     t_enq = time.perf_counter()  # host time to enqueue the steps (the GPU idles if it is ~ ms_per_step)
     ev1.record()
+    if args.spin_sync:
+        while not ev1.query():  # every kernel of the region has completed once the last event has
+            pass
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if use_dist:
@@ -803,6 +812,7 @@ def main():
             "launches_before_window": launches_before if graph is None else None,
             "window_launches": window_launches if graph is None else None,
             "stagger": bool(stagger),
+            "spin_sync": bool(args.spin_sync),
             "higher_is_better": True,
             "scaling": "strong" if args.workload == "c3" else "weak",
             "vs_baseline": None,

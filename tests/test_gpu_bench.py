@@ -92,13 +92,11 @@ def test_bench_line_fails_when_k_step_writes_a_wrong_tag():
     assert rc == 0, line
     assert line["verified"] is True and line["oracle_sample"]["bit_exact"] is True
     assert line["config"]["streams"] == 2 and line["roofline"]["kernel_names"] == ["k_step"]
-    # the staggered two-stream schedule: 2 steps = 2 launches on stream A, Q1 + 1 window + Q2 on stream B
-    assert line["stagger"] is True and line["window_launches"] == 5
-    for steps in ("1", "3"):
-        rc, line = _bench({}, steps)
+    assert line["stagger"] is False and line["window_launches"] == 4 and line["spin_sync"] is True
+    # the staggered two-stream schedule (--stagger 1): 2 steps = 2 launches on stream A, Q1 + 1 window + Q2 on B
+    for steps in ("1", "2", "3"):
+        rc, line = _bench({}, steps, "--stagger", "1")
         assert rc == 0 and line["verified"] is True and line["oracle_sample"]["bit_exact"] is True, line
-        assert line["window_launches"] == 2 * int(steps) + 1
-    rc, line = _bench({}, "2", "--stagger", "0")
-    assert rc == 0 and line["verified"] is True and line["stagger"] is False and line["window_launches"] == 4
+        assert line["stagger"] is True and line["window_launches"] == 2 * int(steps) + 1
     rc, line = _bench({"WG_TEST_STEP_FLIP": "64"})  # the product library: no hook, still bit-exact
     assert rc == 0 and line["verified"] is True and line["oracle_sample"]["bit_exact"] is True

@@ -1192,20 +1192,45 @@ __global__ void __launch_bounds__(LPT_THREADS) k_lpt_scatter(const wg_pkt* d, ui
 template <int MODE>
 __global__ void __launch_bounds__(LPT_THREADS) k_lpt_one(const wg_pkt* d, uint32_t n, uint32_t max_len, uint32_t* cnt,
                                                          uint32_t* cnt_next, uint32_t* order) {
+  // LDS atomics are aggregated per wave and key (a ballot, one atomicAdd by the wave's first lane, ranks by
+  // mbcnt): a few keys shared by 1,024 threads would otherwise serialise on their LDS words
   __shared__ uint32_t h[kFastBins], base[kFastBins];
   if (threadIdx.x < kFastBins) h[threadIdx.x] = 0;
   if (blockIdx.x == 0 && threadIdx.x < kFastBins) cnt_next[threadIdx.x] = 0;
   __syncthreads();
   uint32_t lo, hi;
   lpt_range(n, lo, hi);
-  for (uint32_t i = lo + threadIdx.x; i < hi; i += LPT_THREADS) atomicAdd(&h[lpt_key<MODE>(d, i, max_len)], 1u);
+  const uint32_t lane = threadIdx.x & 63u;
+  auto wave_rank = [&](uint32_t* slots, uint32_t key) {  // this lane's rank among the wave's lanes of its key
+    uint32_t r = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kFastBins; ++k) {
+      const uint64_t m = __ballot(key == k);
+      if (m) {
+        uint32_t b = 0;
+        if (lane == (uint32_t)__builtin_ctzll(m)) b = atomicAdd(&slots[k], (uint32_t)__popcll(m));
+        b = __shfl(b, (int)__builtin_ctzll(m), 64);
+        if (key == k) r = b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+      }
+    }
+    return r;
+  };
+  for (uint32_t i0 = lo; i0 < hi; i0 += LPT_THREADS) {  // every lane of a wave takes part in each trip
+    const uint32_t i = i0 + threadIdx.x;
+    (void)wave_rank(h, i < hi ? lpt_key<MODE>(d, i, max_len) : kFastBins);
+  }
   __syncthreads();
   if (threadIdx.x < kFastBins) {
     const uint32_t k = threadIdx.x, c = h[k];
     base[k] = k * n + (c ? atomicAdd(&cnt[k], c) : 0u);
   }
   __syncthreads();
-  for (uint32_t i = lo + threadIdx.x; i < hi; i += LPT_THREADS) order[atomicAdd(&base[lpt_key<MODE>(d, i, max_len)], 1u)] = i;
+  for (uint32_t i0 = lo; i0 < hi; i0 += LPT_THREADS) {
+    const uint32_t i = i0 + threadIdx.x;
+    const uint32_t key = i < hi ? lpt_key<MODE>(d, i, max_len) : kFastBins;
+    const uint32_t at = wave_rank(base, key);
+    if (i < hi) order[at] = i;
+  }
 }
 
 // ---- wire framing (TransportPacket.java:18-35) --------------------------------------------
