@@ -26,8 +26,13 @@ tail -1 $O/gpu_tests.log
 step smoke
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || die smoke $?
 tail -1 $O/smoke.log
-step "bench c1 (step)"
-timeout -k 10 400 python bench.py > $O/bench_c1.json 2> $O/bench.err || die bench_c1 $?
+step "bench c1: the driver's command (--gpus 1 --steps 20 --warmup 5), three times"
+for i in 1 2 3; do
+  timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_c1_driver$i.json 2>> $O/bench.err || die bench_c1_driver $?
+done
+cat $O/bench_c1_driver1.json
+step "bench c1 (step, 200 steps)"
+timeout -k 10 400 python bench.py > $O/bench_c1.json 2>> $O/bench.err || die bench_c1 $?
 cat $O/bench_c1.json
 timeout -k 10 400 python bench.py > $O/bench_c1b.json 2>> $O/bench.err || die bench_c1b $?
 step "bench c1 under torchrun (RCCL group of one rank)"
@@ -39,6 +44,9 @@ timeout -k 10 300 python bench.py --variant 1 --no-cpu-baseline > $O/bench_c1_st
 step "bench c2"
 timeout -k 10 300 python bench.py --workload c2 > $O/bench_c2.json 2>> $O/bench.err || die bench_c2 $?
 cat $O/bench_c2.json
+step "bench imix"
+timeout -k 10 300 python bench.py --workload imix > $O/bench_imix.json 2>> $O/bench.err || die bench_imix $?
+cat $O/bench_imix.json
 step "bench c3"
 timeout -k 10 400 python bench.py --workload c3 --no-cpu-baseline --steps 5 --warmup 1 > $O/bench_c3.json 2>> $O/bench.err || die bench_c3 $?
 cat $O/bench_c3.json
@@ -63,8 +71,8 @@ fi
 cd /tmp && export TMPDIR=/tmp
 # c1s: C1 with one stream per step (--streams 1): the launch the line's roofline (kernel_ms, frac, traffic)
 # describes; c1: the default two-stream step (the line's value); c2: one stream by default
-for w in c1s c1 c2; do
-  wl=${w%s}; xs=""; [ $w = c1s ] && xs="--streams 1"
+for w in c1s c1 c2 imix; do
+  wl=${w%s}; xs=""; [ $w = c1s ] && xs="--streams 1"; [ $w = imix ] && wl=imix
   step "rocprofv3 kernel trace $w"
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_$w -o run --output-format csv -- python3 $ROOT/bench.py --workload $wl $xs --no-cpu-baseline > $O/prof_bench_$w.json 2> $O/prof_$w.log || die prof_$w $?
   python3 $ROOT/tools/prof_window.py trace $(find $O/prof_$w -name "run_kernel_trace.csv" | head -1) $O/prof_bench_$w.json --out $O/window_$w.json > /dev/null || die window_$w $?
