@@ -100,3 +100,14 @@ def test_bench_line_fails_when_k_step_writes_a_wrong_tag():
         assert line["stagger"] is True and line["window_launches"] == 2 * int(steps) + 1
     rc, line = _bench({"WG_TEST_STEP_FLIP": "64"})  # the product library: no hook, still bit-exact
     assert rc == 0 and line["verified"] is True and line["oracle_sample"]["bit_exact"] is True
+
+
+def test_bench_imix_fused_planning_is_verified():
+    """WG_LPT_FUSED=1 (A/B knob, off by default): the IMIX step's short-packet plan made by the step launch's
+    own first workgroups (k_step_mixed_fused) while the others wait on its publication count, with each poll
+    kind (WG_FUSED_POLL 0/1/2) and planner count (WG_FUSED_NP): every packet must still round-trip and the
+    oracle sample be bit-exact, as on the default two-launch plan."""
+    for env in ({}, {"WG_LPT_FUSED": "1"}, {"WG_LPT_FUSED": "1", "WG_FUSED_POLL": "2", "WG_FUSED_NP": "256"},
+                {"WG_LPT_FUSED": "1", "WG_FUSED_POLL": "1", "WG_FUSED_NP": "7"}):
+        rc, line = _bench(env, "3", "--workload", "imix")
+        assert rc == 0 and line["verified"] is True and line["oracle_sample"]["bit_exact"] is True, (env, line)

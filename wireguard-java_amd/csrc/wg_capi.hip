@@ -132,6 +132,14 @@ struct wg_ctx {
   bool stitch = false;
   // the short-packet split plan's order in one launch (k_lpt_one; WG_LPT_ONE=0: k_lpt_hist + k_lpt_scatter)
   bool lpt_one = true;
+  // WG_LPT_FUSED=1 (A/B, off): in a k_step_mixed step, planned by the step launch's first workgroups
+  // (k_step_mixed_fused) instead of k_lpt_one's own launch. IMIX 66-70 us per step against 59: the planners
+  // take 6-8 us while every other workgroup waits, more than the launch gap they remove
+  // (profiles/r06_fused_ab.jsonl). plan_err: a pinned word the fused kernel sets when a workgroup's wait for
+  // the plan ran out (a later step then fails with WG_EDEVICE)
+  bool lpt_fused = false;
+  uint32_t fused_poll = 0, fused_np = 0;  // WG_FUSED_POLL (k_step_mixed_fused's poll kind), WG_FUSED_NP (planners)
+  uint32_t* plan_err = nullptr;
   // test hook WG_TEST_STEP_FLIP=N (power of two): the k_step launch's seal half writes a wrong tag for every
   // packet whose index is a multiple of N (tests/test_gpu_bench.py: the bench must report verified false)
   uint32_t test_flip = 0;
@@ -383,8 +391,10 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
                    uint64_t cap_waves, uint32_t G, DevBuf& lpt_hist, DevBuf& lpt_order, wgt::TransportParams* Pout,
                    uint32_t* grid_out, bool* ordered_out, const wgt::RxTables* rx = nullptr,
                    bool private_ws = false, bool reuse_order = false, uint32_t split = 0,
-                   uint32_t* claim = nullptr, uint32_t claim_nc = 0) {
+                   uint32_t* claim = nullptr, uint32_t claim_nc = 0, bool* defer_one = nullptr) {
   bool ordered = false;
+  const bool may_defer = defer_one && *defer_one;
+  if (defer_one) *defer_one = false;
   wgt::TransportParams P{};
   P.desc = desc;
   P.n = n;
@@ -459,20 +469,24 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
     const bool one = mixed && max_len <= 2048u && !claim && c->lpt_one;
     if (!reuse_order && one) {
       int rc;
-      if ((rc = lpt_hist.ensure(2 * 8 * sizeof(uint32_t))) != WG_OK) return rc;
+      if ((rc = lpt_hist.ensure(2 * wgt::kPlanSet * sizeof(uint32_t))) != WG_OK) return rc;
       if ((rc = lpt_order.ensure(sizeof(uint32_t) * wgt::kFastBins * (size_t)n)) != WG_OK) return rc;
       if (!private_ws && (rc = ws_acquire(c, s)) != WG_OK) return rc;
       if (!lpt_hist.zeroed) {  // a new buffer, or one the two-launch planner wrote histograms into
-        HIPTRY(hipMemsetAsync(lpt_hist.p, 0, 2 * 8 * sizeof(uint32_t), s));
+        HIPTRY(hipMemsetAsync(lpt_hist.p, 0, 2 * wgt::kPlanSet * sizeof(uint32_t), s));
         lpt_hist.zeroed = true;
         lpt_hist.par = 0;
       }
-      uint32_t* cnt = (uint32_t*)lpt_hist.p + 8u * lpt_hist.par;
-      uint32_t* nxt = (uint32_t*)lpt_hist.p + 8u * (lpt_hist.par ^ 1u);
+      uint32_t* cnt = (uint32_t*)lpt_hist.p + wgt::kPlanSet * lpt_hist.par;
+      uint32_t* nxt = (uint32_t*)lpt_hist.p + wgt::kPlanSet * (lpt_hist.par ^ 1u);
       const uint32_t lgrid = std::max<uint32_t>(1u, std::min<uint32_t>(wgt::LPT_MAX_BLOCKS, (n + 1023u) / 1024u));
-      hipLaunchKernelGGL((wgt::k_lpt_one<MODE>), dim3(lgrid), dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len, cnt, nxt,
-                         (uint32_t*)lpt_order.p);
-      HIPTRY(hipGetLastError());
+      if (may_defer) {  // the caller's k_step_mixed_fused launch plans (into cnt / nxt, as below)
+        *defer_one = true;
+      } else {
+        hipLaunchKernelGGL((wgt::k_lpt_one<MODE>), dim3(lgrid), dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len, cnt,
+                           nxt, (uint32_t*)lpt_order.p);
+        HIPTRY(hipGetLastError());
+      }
       lpt_hist.last_cnt = cnt;
       lpt_hist.par ^= 1u;
     } else if (!reuse_order) {
@@ -687,13 +701,25 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
     // per slot (the same test plan_transport makes for its longest-first pairs); up to 64 sub-orders,
     // plan_transport picks how many divide its grid
     uint32_t claim_nc = 0;
+    if (c->plan_err && __atomic_load_n(c->plan_err, __ATOMIC_ACQUIRE))
+      return fail(WG_EDEVICE, "a k_step_mixed_fused workgroup timed out waiting for its plan");
+    // the short-packet plan folded into the step launch (k_step_mixed_fused): a pinned error word first
+    bool defer = c->lpt_fused && !c->stitch;
+    if (defer && !c->plan_err) {
+      void* p = nullptr;
+      if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess || !p) defer = false;
+      else {
+        memset(p, 0, 64);
+        c->plan_err = (uint32_t*)p;
+      }
+    }
     if (c->claim && !(sb->flags & WG_F_UNIFORM) && sp.split == 0 && G == 8 && 2ull * sb->n > 8ull * cap &&
         c->lpt_claim.ensure(64u * 64u) == WG_OK && c->lpt_chain.ensure(sizeof(uint2) * (size_t)sb->n) == WG_OK)
       claim_nc = 64;
     rc = plan_transport<WG_MODE_SEAL>(c, sb->desc, sb->n, sb->in, sb->in_size, sb->out, sb->out_size, nullptr,
                                       sb->max_len, sb->flags, s, cap, G, c->lpt_hist, c->lpt_order, &PS, &gs, &os,
                                       nullptr, true, false, sp.split, claim_nc ? (uint32_t*)c->lpt_claim.p : nullptr,
-                                      claim_nc);
+                                      claim_nc, &defer);
     if (rc == WG_OK)
       rc = plan_transport<WG_MODE_OPEN>(c, ob->desc, ob->n, ob->in, ob->in_size, ob->out, ob->out_size, ob->status,
                                         ob->max_len, ob->flags & ~WG_F_AFTER_SEAL, s, cap, G, c->lpt_hist,
@@ -713,7 +739,20 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
     if (rc == WG_OK) {
       hipEvent_t ev;
       record_start(c, s, &ev);
-      if (claim_nc) hipLaunchKernelGGL((wgt::k_step_claim<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+      if (defer) {  // the planner's blocks first (as k_lpt_one's grid, with 64 x TW threads each), then the step's
+        uint32_t np = std::max<uint32_t>(1u, std::min<uint32_t>(wgt::LPT_MAX_BLOCKS, (sb->n + 1023u) / 1024u));
+        if (c->fused_np) np = std::min<uint32_t>(c->fused_np, std::max<uint32_t>(1u, sb->n / 256u));
+        uint32_t* cnt = const_cast<uint32_t*>(PS.bin_cnt);
+        uint32_t* nxt = (uint32_t*)c->lpt_hist.p + wgt::kPlanSet * c->lpt_hist.par;  // plan_transport flipped par
+        uint32_t* err = nullptr;
+        HIPTRY(hipHostGetDevicePointer((void**)&err, c->plan_err, 0));
+        if (sp.gs == 4)
+          hipLaunchKernelGGL(wgt::k_step_mixed_fused<4>, dim3(np + gs), dim3(64 * wgt::TW), 0, s, PS, PO, np, cnt, nxt, err,
+                             c->fused_poll);
+        else
+          hipLaunchKernelGGL(wgt::k_step_mixed_fused<8>, dim3(np + gs), dim3(64 * wgt::TW), 0, s, PS, PO, np, cnt, nxt, err,
+                             c->fused_poll);
+      } else if (claim_nc) hipLaunchKernelGGL((wgt::k_step_claim<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else if (PS.n_long && sp.gs == 4 && c->stitch)
         hipLaunchKernelGGL((wgt::k_step_mixed<4, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else if (PS.n_long && sp.gs == 4) hipLaunchKernelGGL(wgt::k_step_mixed<4>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
@@ -855,6 +894,9 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   if (const char* e = getenv("WG_CLAIM")) c->claim = atoi(e) != 0;
   if (const char* e = getenv("WG_STITCH")) c->stitch = atoi(e) != 0;
   if (const char* e = getenv("WG_LPT_ONE")) c->lpt_one = atoi(e) != 0;
+  if (const char* e = getenv("WG_LPT_FUSED")) c->lpt_fused = atoi(e) != 0;
+  if (const char* e = getenv("WG_FUSED_POLL")) c->fused_poll = (uint32_t)std::max(0, atoi(e));
+  if (const char* e = getenv("WG_FUSED_NP")) c->fused_np = (uint32_t)std::max(0, atoi(e));
 #ifdef WG_TEST_HOOKS
   // fault-injection hooks exist only in the test library (make test: libwgaead_test.so); the product
   // library never reads these variables, so no environment can make it write wrong tags
@@ -890,6 +932,7 @@ int wg_ctx_destroy(wg_ctx* c) {
                     &c->lpt_order, &c->lpt_hist2, &c->lpt_order2, &c->lpt_nlong, &c->h_desc, &c->h_in, &c->h_out, &c->h_aad, &c->h_status,
                     &c->h_keys})
     b->release();
+  if (c->plan_err) (void)hipHostFree(c->plan_err);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->copy_out_stream) (void)hipStreamDestroy(c->copy_out_stream);

@@ -1183,24 +1183,27 @@ __global__ void __launch_bounds__(LPT_THREADS) k_lpt_scatter(const wg_pkt* d, ui
   for (uint32_t i = lo + threadIdx.x; i < hi; i += LPT_THREADS) order[atomicAdd(&base[lpt_key<MODE>(d, i, max_len)], 1u)] = i;
 }
 
-// One launch instead of k_lpt_hist + k_lpt_scatter, for batches whose keys fit kFastBins (max_len <= 2,048 B,
-// the short-packet plan): each block counts its range's keys in LDS, takes its base in every non-empty key
-// with ONE atomicAdd on that key's global counter, and ranks its packets into the key's region of a sparse
-// order (key k at order[k * n]). No grid-wide barrier: the consumer derives the positions from the counts.
-// The counters are double-buffered by call (cnt for this call, zero on entry; cnt_next zeroed here for the
-// next), so no memset launch either. Order inside a key: arbitrary (every position of the order is a packet).
-template <int MODE>
-__global__ void __launch_bounds__(LPT_THREADS) k_lpt_one(const wg_pkt* d, uint32_t n, uint32_t max_len, uint32_t* cnt,
-                                                         uint32_t* cnt_next, uint32_t* order) {
-  // LDS atomics are aggregated per wave and key (a ballot, one atomicAdd by the wave's first lane, ranks by
-  // mbcnt): a few keys shared by 1,024 threads would otherwise serialise on their LDS words
-  __shared__ uint32_t h[kFastBins], base[kFastBins];
+// k_lpt_one's counter set: 64 words per call (counts at [0, kFastBins), the fused step's publication count at
+// kPlanDone), two sets used in turn
+constexpr uint32_t kPlanSet = 64, kPlanDone = 32;
+
+// The body of k_lpt_one for block `blk` of `nblk` with `threads` threads: h / base are kFastBins words of LDS.
+// A thread takes KPT packets per trip, their descriptor loads issued together, and when the block's range is
+// one trip (the usual case) keeps the keys for the scatter pass: two load latencies per plan, not 2 x trips.
+template <int MODE, int KPT = 1>
+__device__ __forceinline__ void lpt_one_body(const wg_pkt* d, uint32_t n, uint32_t max_len, uint32_t* cnt,
+                                             uint32_t* cnt_next, uint32_t* order, uint32_t blk, uint32_t nblk,
+                                             uint32_t threads, uint32_t* h, uint32_t* base) {
   if (threadIdx.x < kFastBins) h[threadIdx.x] = 0;
-  if (blockIdx.x == 0 && threadIdx.x < kFastBins) cnt_next[threadIdx.x] = 0;
+  // the next call's counts ([0, kFastBins)) and k_step_mixed_fused's publication count (kPlanDone: its own line,
+  // away from the counts' atomics)
+  if (blk == 0 && (threadIdx.x < 8u || threadIdx.x == kPlanDone)) cnt_next[threadIdx.x] = 0;
   __syncthreads();
-  uint32_t lo, hi;
-  lpt_range(n, lo, hi);
-  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t per = (n + nblk - 1u) / nblk;
+  const uint32_t lo = min(n, blk * per), hi = min(n, lo + per);
+  const uint32_t lane = threadIdx.x & 63u, span = threads * KPT;
+  // LDS atomics are aggregated per wave and key (a ballot, one atomicAdd by the wave's first lane, ranks by
+  // mbcnt): a few keys shared by all threads would otherwise serialise on their LDS words
   auto wave_rank = [&](uint32_t* slots, uint32_t key) {  // this lane's rank among the wave's lanes of its key
     uint32_t r = 0;
 #pragma unroll
@@ -1215,9 +1218,18 @@ __global__ void __launch_bounds__(LPT_THREADS) k_lpt_one(const wg_pkt* d, uint32
     }
     return r;
   };
-  for (uint32_t i0 = lo; i0 < hi; i0 += LPT_THREADS) {  // every lane of a wave takes part in each trip
-    const uint32_t i = i0 + threadIdx.x;
-    (void)wave_rank(h, i < hi ? lpt_key<MODE>(d, i, max_len) : kFastBins);
+  auto keys_at = [&](uint32_t i0, uint32_t (&key)[KPT]) {  // every lane of a wave takes part in each trip
+#pragma unroll
+    for (int t = 0; t < KPT; ++t) {
+      const uint32_t i = i0 + t * threads + threadIdx.x;
+      key[t] = i < hi ? lpt_key<MODE>(d, i, max_len) : kFastBins;
+    }
+  };
+  uint32_t key[KPT];
+  for (uint32_t i0 = lo; i0 < hi; i0 += span) {
+    keys_at(i0, key);
+#pragma unroll
+    for (int t = 0; t < KPT; ++t) (void)wave_rank(h, key[t]);
   }
   __syncthreads();
   if (threadIdx.x < kFastBins) {
@@ -1225,12 +1237,117 @@ __global__ void __launch_bounds__(LPT_THREADS) k_lpt_one(const wg_pkt* d, uint32
     base[k] = k * n + (c ? atomicAdd(&cnt[k], c) : 0u);
   }
   __syncthreads();
-  for (uint32_t i0 = lo; i0 < hi; i0 += LPT_THREADS) {
-    const uint32_t i = i0 + threadIdx.x;
-    const uint32_t key = i < hi ? lpt_key<MODE>(d, i, max_len) : kFastBins;
-    const uint32_t at = wave_rank(base, key);
-    if (i < hi) order[at] = i;
+  const bool one_trip = hi - lo <= span;
+  for (uint32_t i0 = lo; i0 < hi; i0 += span) {
+    if (!one_trip) keys_at(i0, key);
+#pragma unroll
+    for (int t = 0; t < KPT; ++t) {
+      const uint32_t i = i0 + t * threads + threadIdx.x;
+      const uint32_t at = wave_rank(base, key[t]);
+      if (i < hi) order[at] = i;
+    }
   }
+}
+
+// One launch instead of k_lpt_hist + k_lpt_scatter, for batches whose keys fit kFastBins (max_len <= 2,048 B,
+// the short-packet plan): each block counts its range's keys in LDS, takes its base in every non-empty key
+// with ONE atomicAdd on that key's global counter, and ranks its packets into the key's region of a sparse
+// order (key k at order[k * n]). No grid-wide barrier: the consumer derives the positions from the counts.
+// The counters are double-buffered by call (cnt for this call, zero on entry; cnt_next zeroed here for the
+// next), so no memset launch either. Order inside a key: arbitrary (every position of the order is a packet).
+template <int MODE>
+__global__ void __launch_bounds__(LPT_THREADS) k_lpt_one(const wg_pkt* d, uint32_t n, uint32_t max_len, uint32_t* cnt,
+                                                         uint32_t* cnt_next, uint32_t* order) {
+  __shared__ uint32_t h[kFastBins], base[kFastBins];
+  lpt_one_body<MODE>(d, n, max_len, cnt, cnt_next, order, blockIdx.x, gridDim.x, LPT_THREADS, h, base);
+}
+
+// k_step_mixed with its planning folded in (WG_LPT_FUSED, the short-packet plan): workgroups [0, np) plan as
+// k_lpt_one does and then publish (their stores acknowledged, one release count per workgroup in cnt[kPlanDone]); the
+// other workgroups wait for all np publications (one acquire poll per workgroup, s_sleep between polls) and
+// then run k_step_mixed's body. The planners are the lowest workgroup indices, so they are dispatched before
+// any waiting workgroup can occupy the machine. A wait is bounded (kPlanWaitTicks of s_memrealtime); a
+// workgroup that runs out of it writes *err and does no work, and the host fails the next call.
+constexpr uint64_t kPlanWaitTicks = 5000000;  // 50 ms at 100 MHz
+#ifdef WG_DIAG  // diagnostic build: s_memrealtime per workgroup (tools/fused_timing.py): a planner's start and
+                // publication, a consumer's arrival, release from the wait and end
+constexpr size_t kFusedStampOff = 400000;
+#define WG_FUSED_STAMP(j, v) \
+  if (S.stamps && threadIdx.x == 0) S.stamps[kFusedStampOff + 3u * blockIdx.x + (j)] = (v)
+#else
+#define WG_FUSED_STAMP(j, v)
+#endif
+template <int GS = 8, bool ST = false>
+__global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(ST ? WG_STITCH_WPE : 8)))
+k_step_mixed_fused(TransportParams S, TransportParams O, uint32_t np, uint32_t* cnt, uint32_t* cnt_next, uint32_t* err,
+                   uint32_t poll) {
+  __shared__ uint4 img_[TW][4 * 64];
+  __shared__ SlotRec rec_[TW][64 / GS];
+  WG_FUSED_STAMP(0, __builtin_amdgcn_s_memrealtime());
+  if (blockIdx.x < np) {
+    uint32_t* h = (uint32_t*)&img_[0][0];
+    lpt_one_body<WG_MODE_SEAL, 4>(S.desc, S.n, S.max_len, cnt, cnt_next, (uint32_t*)S.order, blockIdx.x, np, 64u * TW,
+                               h, h + 8);
+    // every wave's order stores acknowledged by its L2, then one release (one L2 write-back) per workgroup
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(&cnt[kPlanDone], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    WG_FUSED_STAMP(1, __builtin_amdgcn_s_memrealtime());
+    return;
+  }
+  __shared__ uint32_t go;
+  if (threadIdx.x == 0) {
+    uint32_t ok = 1u;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    // relaxed polls (an acquire per poll would invalidate the L2 every time), one acquire fence after
+    // poll (WG_FUSED_POLL, A/B): 0 agent-scope loads, 1 system-scope loads, 2 read-modify-writes (performed at
+    // the coherence point), at a quarter of the rate
+    auto published = [&]() {
+      if (poll == 1) return __hip_atomic_load(&cnt[kPlanDone], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (poll == 2) return __hip_atomic_fetch_add(&cnt[kPlanDone], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return __hip_atomic_load(&cnt[kPlanDone], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    while (published() < np) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kPlanWaitTicks) {
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ok = 0u;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);  // ~0.2 us: the polls of every waiting workgroup meet at one line
+      if (poll == 2) {
+        __builtin_amdgcn_s_sleep(8);
+        __builtin_amdgcn_s_sleep(8);
+        __builtin_amdgcn_s_sleep(8);
+      }
+    }
+    // no agent-scope acquire here: its L2 invalidation, made by every waiting workgroup at about the same time,
+    // cost the step 28 us (IMIX, profiles/r06_fused_ab.jsonl). None is needed on this hardware path: the plan's
+    // lines cannot be in this XCD's L2 (a dispatch starts with the L2s invalidated, and no workgroup of this
+    // launch reads them before the plan is published: the planners only write them, by stores and by atomics
+    // performed at the device's coherence point), and the planners' release wrote them back; only this CU's
+    // L1 is invalidated, as between a step's halves
+    asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
+    go = ok;
+    WG_FUSED_STAMP(1, __builtin_amdgcn_s_memrealtime());
+  }
+  __syncthreads();
+  if (!go) return;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  TransportParams QS, QO;
+  uint32_t qb = 0, qb2 = 0, iter = 0;
+  const uint32_t blk = blockIdx.x - np;
+  const int g = mixed_part<GS>(S, blk, QS, qb);
+  (void)mixed_part<GS>(O, blk, QO, qb2);
+  if (g == 16) {
+    transport_body<WG_MODE_SEAL, 16, false, kPosStatic, ST, true>(QS, qb, wv, img_[wv], rec_[wv], iter);
+    asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
+    transport_body<WG_MODE_OPEN, 16, false, kPosStatic, ST, true>(QO, qb, wv, img_[wv], rec_[wv], iter);
+  } else if (g == GS) {
+    transport_body<WG_MODE_SEAL, GS, false, kPosStatic, ST, true>(QS, qb, wv, img_[wv], rec_[wv], iter);
+    asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
+    transport_body<WG_MODE_OPEN, GS, false, kPosStatic, ST, true>(QO, qb, wv, img_[wv], rec_[wv], iter);
+  }
+  WG_FUSED_STAMP(2, __builtin_amdgcn_s_memrealtime());
 }
 
 // ---- wire framing (TransportPacket.java:18-35) --------------------------------------------
