@@ -423,3 +423,62 @@ def test_mixed_batch_on_two_streams_shares_plan_workspace(engine):
     torch.cuda.synchronize()
     for (out, _, _), ref in zip(outs, refs):
         assert np.array_equal(out.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("slot2,workload", [(1, "imix"), (2, "imix"), (0, "ragged"), (1, "ragged"), (2, "ragged")])
+def test_two_lane_slots_every_packet(slot2, workload):
+    """WG_SLOT2=k (default 1): the short-packet split plan's step (k_step_mixed<4, false, 2>) puts the packets
+    of at most 8 k blocks (keys <= k) in 2-lane slots, after the 16-lane and 4-lane parts (0: no 2-lane part,
+    k_step_mixed<4>). 80-B slot records, the key read from the key table each round. "imix" is bench.py's IMIX
+    batch; "ragged" is 65,536 packets of 0..2,048 B (every partial-chunk shape in 2-lane slots, empty
+    packets, and both other parts populated). Two steps in a row: every ct || tag against the oracle, every
+    plaintext back, every status OK."""
+    import os
+
+    import bench
+    torch, dev = _dev()
+    W = wg()
+    old = os.environ.get("WG_SLOT2")
+    os.environ["WG_SLOT2"] = str(slot2)
+    try:
+        eng = W.Engine(0, key_slots=256)
+    finally:
+        if old is None:
+            del os.environ["WG_SLOT2"]
+        else:
+            os.environ["WG_SLOT2"] = old
+    try:
+        if workload == "imix":
+            lengths, slots, counters, nkeys, _, _ = bench.build_workload("imix", 0, 1)
+        else:
+            n = 65536
+            lengths = (splitmix_np(0x5107 + slot2, 4 * n).view("<u4") % 2049).astype(np.int64)
+            lengths[:64] = np.arange(64)  # 0..63 B: every partial first block
+            slots, counters, nkeys = np.arange(n) % 256, np.arange(n, dtype=np.uint64) // 256, 256
+        n = len(lengths)
+        S = ((lengths + 16 + 15) // 16) * 16
+        off = np.concatenate([[0], np.cumsum(S)[:-1]]).astype(np.uint64)
+        total = int(S.sum())
+        desc = W.pack_desc(off, off, counters, lengths, slots)
+        keys = splitmix_np(0x2A2E + slot2, 32 * nkeys)
+        pt = splitmix_np(0x5EED2029 + slot2, total)
+        eng.set_keys(0, keys.tobytes())
+        ml = int(lengths.max())
+        d = torch.from_numpy(W.desc_as_int64(desc)).to(dev)
+        dpt = torch.from_numpy(pt).to(dev)
+        ref = np.zeros(total, np.uint8)
+        O.seal_batch(desc, pt, ref, keys, threads=16)
+        want = pt.copy()
+        for i in range(n):
+            want[int(off[i]) + int(lengths[i]):int(off[i]) + int(S[i])] = 0  # slack: never written
+        for _ in range(2):
+            dct = torch.zeros(total, dtype=torch.uint8, device=dev)
+            back = torch.zeros(total, dtype=torch.uint8, device=dev)
+            st = torch.full((n,), 7, dtype=torch.int32, device=dev)
+            eng.duplex(d, dpt, dct, ml, d, dct, back, st, ml, uniform=False, after_seal=True)
+            torch.cuda.synchronize()
+            assert np.array_equal(dct.cpu().numpy(), ref)
+            assert int(st.abs().sum().item()) == 0
+            assert np.array_equal(back.cpu().numpy(), want)
+    finally:
+        eng.close()

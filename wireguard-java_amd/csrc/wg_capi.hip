@@ -138,6 +138,11 @@ struct wg_ctx {
   // (profiles/r06_fused_ab.jsonl). plan_err: a pinned word the fused kernel sets when a workgroup's wait for
   // the plan ran out (a later step then fails with WG_EDEVICE)
   bool lpt_fused = false;
+  // the short-packet split plan's tiny packets (keys <= slot2, i.e. at most 8 x slot2 blocks: 448 B for 1) in
+  // 2-lane slots (k_step_mixed<4, false, 2>; WG_SLOT2=k, 0: none). IMIX +2.3% (715 -> 731 GiB/s, three
+  // alternations); 65,536 x 40 B 37.0 -> 27.1 us per step; 2 (576-B packets too) measured +-0
+  // (profiles/r06_slot2_ab.jsonl)
+  uint32_t slot2 = 1;
   uint32_t fused_poll = 0, fused_np = 0;  // WG_FUSED_POLL (k_step_mixed_fused's poll kind), WG_FUSED_NP (planners)
   uint32_t* plan_err = nullptr;
   // test hook WG_TEST_STEP_FLIP=N (power of two): the k_step launch's seal half writes a wrong tag for every
@@ -755,7 +760,10 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
       } else if (claim_nc) hipLaunchKernelGGL((wgt::k_step_claim<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else if (PS.n_long && sp.gs == 4 && c->stitch)
         hipLaunchKernelGGL((wgt::k_step_mixed<4, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
-      else if (PS.n_long && sp.gs == 4) hipLaunchKernelGGL(wgt::k_step_mixed<4>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+      else if (PS.n_long && sp.gs == 4 && PS.bin_cnt && c->slot2 && c->slot2 < sp.split && c->key_slots < (1u << 24)) {
+        PS.split2 = PO.split2 = c->slot2;  // a third part: the grid's upper bound grows by one workgroup
+        hipLaunchKernelGGL((wgt::k_step_mixed<4, false, 2>), dim3(gs + 1), dim3(64 * wgt::TW), 0, s, PS, PO);
+      } else if (PS.n_long && sp.gs == 4) hipLaunchKernelGGL(wgt::k_step_mixed<4>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else if (PS.n_long && c->stitch)
         hipLaunchKernelGGL((wgt::k_step_mixed<8, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else if (PS.n_long) hipLaunchKernelGGL(wgt::k_step_mixed<8>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
@@ -895,6 +903,7 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   if (const char* e = getenv("WG_STITCH")) c->stitch = atoi(e) != 0;
   if (const char* e = getenv("WG_LPT_ONE")) c->lpt_one = atoi(e) != 0;
   if (const char* e = getenv("WG_LPT_FUSED")) c->lpt_fused = atoi(e) != 0;
+  if (const char* e = getenv("WG_SLOT2")) c->slot2 = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_FUSED_POLL")) c->fused_poll = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_FUSED_NP")) c->fused_np = (uint32_t)std::max(0, atoi(e));
 #ifdef WG_TEST_HOOKS

@@ -184,6 +184,22 @@ __device__ __forceinline__ void chacha20_block_hoisted(const uint4* key_lds, uin
   out[8] = x8 + kb.x; out[9] = x9 + kb.y; out[10] = x10 + kb.z; out[11] = x11 + kb.w;
   out[12] = x12 + ctr; out[13] = x13 + n0; out[14] = x14 + n1; out[15] = x15 + n2;
 }
+// A whole block without the hoisted first column round (2-lane slots, which have no lanes to compute it on
+// for the others): the same placed asm over all 20 rounds, then the feed-forward.
+__device__ __forceinline__ void chacha20_block_full(const uint4* key_lds, uint32_t ctr, uint32_t n0, uint32_t n1,
+                                                    uint32_t n2, uint32_t out[16]) {
+  uint4 ka = key_lds[0], kb = key_lds[1];
+  uint32_t y[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, ka.x, ka.y, ka.z, ka.w,
+                    kb.x,        kb.y,        kb.z,        kb.w,        ctr,  n0,   n1,   n2};
+  chacha20_rounds_asm(y);
+  asm volatile("" ::: "memory");
+  ka = key_lds[0];
+  kb = key_lds[1];
+  out[0] = y[0] + 0x61707865u; out[1] = y[1] + 0x3320646eu; out[2] = y[2] + 0x79622d32u; out[3] = y[3] + 0x6b206574u;
+  out[4] = y[4] + ka.x; out[5] = y[5] + ka.y; out[6] = y[6] + ka.z; out[7] = y[7] + ka.w;
+  out[8] = y[8] + kb.x; out[9] = y[9] + kb.y; out[10] = y[10] + kb.z; out[11] = y[11] + kb.w;
+  out[12] = y[12] + ctr; out[13] = y[13] + n0; out[14] = y[14] + n1; out[15] = y[15] + n2;
+}
 #undef WG_QR
 #undef WG_QR_SDWA
 

@@ -132,6 +132,7 @@ struct TransportParams {
   uint32_t bin_cap;
   uint32_t pos_base;
   uint32_t split;
+  uint32_t split2;  // k_step_mixed with GT = 2: keys <= split2 (> 0) take 2-lane slots, after the GS-lane part
   // dynamic claims (k_step_claim, mixed-length batches): the longest-first order is dealt
   // as claim_nc interleaved sub-orders (positions c, c + nc, c + 2 nc, ...), sub-order c to the workgroups
   // b with b % nc == c; each slot starts on a static position and claims every later one from its
@@ -180,7 +181,7 @@ struct TransportParams {
 // ds_swizzle bitmask mode inside each 32-lane half: src = ((lane & and) | or) ^ xor.
 template <int G, int K>
 __device__ __forceinline__ uint32_t bcastg(uint32_t v) {  // every lane of the slot reads lane K of it
-  static_assert(G == 4 || G == 8 || G == 16, "slots of 4, 8 or 16 lanes");
+  static_assert(G == 2 || G == 4 || G == 8 || G == 16, "slots of 2, 4, 8 or 16 lanes");
   return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (0x20 - G) | (K << 5));
 }
 template <int K>
@@ -191,15 +192,19 @@ __device__ __forceinline__ uint32_t xorg(uint32_t v) {  // lane reads lane ^ X (
 }
 
 // A slot's copy of one 32-B descriptor (wg_pkt = 8 dwords): with 8 or 16 lanes, lane j holds dword j & 7
-// (w0); with 4 lanes, lane j holds dwords 2j and 2j + 1 (w0, w1: one 8-B load, desc_load4). desc_word<G, K>
-// gives every lane of the slot dword K.
+// (w.x); with 4 lanes, lane j holds dwords 2j and 2j + 1 (w.x, w.y: one 8-B load, desc_load4); with 2 lanes,
+// dwords 4j .. 4j + 3 (one 16-B load, desc_load2). desc_word<G, K> gives every lane of the slot dword K.
 __device__ __forceinline__ uint2 desc_load4(const wg_pkt* d, uint32_t i, uint32_t j) {
   return i != ~0u ? ((const uint2*)(d + i))[j & 3u] : make_uint2(0u, 0u);
 }
+__device__ __forceinline__ uint4 desc_load2(const wg_pkt* d, uint32_t i, uint32_t j) {
+  return i != ~0u ? ((const uint4*)(d + i))[j & 1u] : make_uint4(0u, 0u, 0u, 0u);
+}
 template <int G, int K>
-__device__ __forceinline__ uint32_t desc_word(uint32_t w0, uint32_t w1) {
-  if constexpr (G == 4) return bcastg<4, K / 2>((K & 1) ? w1 : w0);
-  else return bcastg<G, K>(w0);
+__device__ __forceinline__ uint32_t desc_word(const uint4& w) {
+  if constexpr (G == 2) return bcastg<2, K / 4>((K & 3) == 0 ? w.x : (K & 3) == 1 ? w.y : (K & 3) == 2 ? w.z : w.w);
+  else if constexpr (G == 4) return bcastg<4, K / 2>((K & 1) ? w.y : w.x);
+  else return bcastg<G, K>(w.x);
 }
 
 // The same exchanges through DPP (VALU, no LDS round trip) for the dependent chains of the
@@ -382,11 +387,20 @@ template <int MODE, int G = 8, bool VF = false, int PM = kPosStatic, bool ST = f
 __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_t blk, uint32_t wv, uint4* const img,
                                                SlotRec* const rec, uint32_t& iter) {
   static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
-  static_assert(G == 4 || G == 8 || G == 16, "slots of 4, 8 or 16 lanes");
+  static_assert(G == 2 || G == 4 || G == 8 || G == 16, "slots of 2, 4, 8 or 16 lanes");
+  static_assert(G != 2 || (MX && !VF && !ST), "2-lane slots: the short-packet split plan's tiny packets only");
+#ifdef WG_HORNER2
+  static_assert(G != 2, "the two-chunk Horner assumes G >= 4");
+#endif
   static_assert(!VF || MODE == WG_MODE_OPEN, "verify-first is an open variant");
   static_assert(!(ST && VF), "the verify-first open keeps the sequential Horner");
-  constexpr uint32_t SH = G == 4 ? 2u : G == 8 ? 3u : 4u;  // log2 G
+  constexpr uint32_t SH = G == 2 ? 1u : G == 4 ? 2u : G == 8 ? 3u : 4u;  // log2 G
   constexpr uint32_t JM = G - 1u;
+  // a slot's record (SlotRec); 2-lane slots keep an 80-B one, so 32 of them per wave leave the launch at 6
+  // workgroups per CU: no key (read from the key table each round, the slot's key index in meta.w >> 8), no
+  // 5 R limbs (formed where used), s = {R1.y, R1.z, R1.w, R2.x} beside R4 = R1.x
+  constexpr uint32_t kRecStride = G == 2 ? 80u : (uint32_t)sizeof(SlotRec);
+  auto RS = [rec](uint32_t si) -> SlotRec& { return *(SlotRec*)((char*)rec + si * kRecStride); };
   if (P.prio_step && iter == 0) __builtin_amdgcn_s_setprio(3);  // first instruction: a fresh wave is never starved
   const uint32_t S = P.slots;
   uint32_t wg = blk * TW + wv;  // this wave's index in the grid
@@ -416,13 +430,15 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
     npos = pos;
     nxt = pos < P.n ? pkt_at<MX>(P, pos) : ~0u;
   }
-  uint32_t dnext = 0u, dnext2 = 0u;
-  if constexpr (G == 4) {
+  uint4 dn = make_uint4(0u, 0u, 0u, 0u);  // this lane's part of the next descriptor (desc_word)
+  if constexpr (G == 2) {
+    dn = desc_load2(P.desc, nxt, opaque_lane());
+  } else if constexpr (G == 4) {
     const uint2 w = desc_load4(P.desc, nxt, opaque_lane());
-    dnext = w.x;
-    dnext2 = w.y;
+    dn.x = w.x;
+    dn.y = w.y;
   } else {
-    dnext = nxt != ~0u ? ((const uint32_t*)(P.desc + nxt))[opaque_lane() & 7u] : 0u;
+    dn.x = nxt != ~0u ? ((const uint32_t*)(P.desc + nxt))[opaque_lane() & 7u] : 0u;
   }
 
   bool have = false;
@@ -455,12 +471,12 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
       const uint32_t lane = opaque_lane(), s = lane >> SH, j = lane & JM;
       pkt = nxt;
 #ifdef WG_DIAG
-      { uint32_t dn = dnext, dn2 = dnext2; asm volatile("s_waitcnt vmcnt(0)" : "+v"(dn), "+v"(dn2)); dnext = dn; dnext2 = dn2; }
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(dn.x), "+v"(dn.y), "+v"(dn.z), "+v"(dn.w));
       WG_PH(6);
 #endif
-      const uint32_t d0 = desc_word<G, 0>(dnext, dnext2), d1 = desc_word<G, 1>(dnext, dnext2),
-                     d2 = desc_word<G, 2>(dnext, dnext2), d3 = desc_word<G, 3>(dnext, dnext2);
-      const uint32_t len = desc_word<G, 6>(dnext, dnext2), ks = desc_word<G, 7>(dnext, dnext2);
+      const uint32_t d0 = desc_word<G, 0>(dn), d1 = desc_word<G, 1>(dn), d2 = desc_word<G, 2>(dn),
+                     d3 = desc_word<G, 3>(dn);
+      const uint32_t len = desc_word<G, 6>(dn), ks = desc_word<G, 7>(dn);
       const uint64_t in_off = (uint64_t)d0 | ((uint64_t)d1 << 32);
       const uint64_t out_off = (uint64_t)d2 | ((uint64_t)d3 << 32);
       const bool valid =
@@ -489,28 +505,30 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         uint32_t v = k[0];
 #pragma unroll
         for (uint32_t i = 1; i < 8u; ++i) v = j == i ? k[i] : v;
-        if constexpr (G == 4) {  // 4 lanes: key words j and j + 4
+        if constexpr (G == 2) {  // 2 lanes: no key in the record
+        } else if constexpr (G == 4) {  // 4 lanes: key words j and j + 4
           uint32_t v2 = k[4];
 #pragma unroll
           for (uint32_t i = 1; i < 4u; ++i) v2 = j == i ? k[4u + i] : v2;
           if (valid) {
-            ((uint32_t*)rec[s].key)[j] = v;
-            ((uint32_t*)rec[s].key)[j + 4u] = v2;
+            ((uint32_t*)RS(s).key)[j] = v;
+            ((uint32_t*)RS(s).key)[j + 4u] = v2;
           }
         } else if (valid && j < 8u) {
-          ((uint32_t*)rec[s].key)[j] = v;
+          ((uint32_t*)RS(s).key)[j] = v;
         }
+      } else if (G == 2) {
       } else if (valid && G == 4) {
-        ((uint32_t*)rec[s].key)[j] = P.keys[8u * ks + j];
-        ((uint32_t*)rec[s].key)[j + 4u] = P.keys[8u * ks + j + 4u];
+        ((uint32_t*)RS(s).key)[j] = P.keys[8u * ks + j];
+        ((uint32_t*)RS(s).key)[j + 4u] = P.keys[8u * ks + j + 4u];
       } else if (valid && j < 8u) {
-        ((uint32_t*)rec[s].key)[j] = P.keys[8u * ks + j];
+        ((uint32_t*)RS(s).key)[j] = P.keys[8u * ks + j];
       }
       // all lanes active: swizzles read live lanes
-      const uint32_t c0 = desc_word<G, 4>(dnext, dnext2), c1 = desc_word<G, 5>(dnext, dnext2);
+      const uint32_t c0 = desc_word<G, 4>(dn), c1 = desc_word<G, 5>(dn);
       if (j == 0) {
-        rec[s].addr = make_uint4(d0, d1, d2, d3);
-        rec[s].meta = make_uint4(c0, c1, len, (valid ? 1u : 0u) | al);
+        RS(s).addr = make_uint4(d0, d1, d2, d3);
+        RS(s).meta = make_uint4(c0, c1, len, (valid ? 1u : 0u) | al | (G == 2 && valid ? ks << 8 : 0u));
       }
       round = 0;
       have = true;
@@ -533,12 +551,14 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         npos = cn.x;
         nxt = cn.y;
       }
-      if constexpr (G == 4) {
+      if constexpr (G == 2) {
+        dn = desc_load2(P.desc, nxt, j);
+      } else if constexpr (G == 4) {
         const uint2 w = desc_load4(P.desc, nxt, j);
-        dnext = w.x;
-        dnext2 = w.y;
+        dn.x = w.x;
+        dn.y = w.y;
       } else {
-        dnext = nxt != ~0u ? ((const uint32_t*)(P.desc + nxt))[j & 7u] : 0u;
+        dn.x = nxt != ~0u ? ((const uint32_t*)(P.desc + nxt))[j & 7u] : 0u;
       }
     }
     if (!__any(have)) break;
@@ -546,7 +566,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
     WG_PH(0);
 
     // this round's packet parameters, read once (meta = {ctr lo, ctr hi, len, flags})
-    const uint4 meta = rec[opaque_lane() >> SH].meta;
+    const uint4 meta = RS(opaque_lane() >> SH).meta;
     const uint32_t len = meta.z;
     const uint32_t nb = (meta.w & 1u) ? ((len + 63u) >> 6) + 1u : 0u;
     // ST: slots whose previous round (not their packet's last) still owes its Horner steps
@@ -562,7 +582,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
       if (have && b < nb && b > 0u) {
         const uint32_t off = 64u * (b - 1u);
         const uint32_t nbytes = min(64u, len - off);
-        const uint4 ad = rec[s].addr;
+        const uint4 ad = RS(s).addr;
         const uint8_t* src = P.in + (((uint64_t)ad.x | ((uint64_t)ad.y << 32)) + off);
         if (meta.w & 2u) {
           // chunks holding a valid byte, each read whole (an aligned 16-B read stays in the granule
@@ -580,9 +600,9 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
       };
       if (!stitch) payload_dma();
       // ---- ChaCha20: block b = 8 round + j ----------------------------------------------
-      if (__any(have && round == 0)) {  // a new packet: its columns 1..3 of the first round, once
+      if (G > 2 && __any(have && round == 0)) {  // a new packet: its columns 1..3 of the first round, once
         const uint32_t c = j & 3u;
-        const uint4* kl = rec[s].key;
+        const uint4* kl = RS(s).key;
         const uint4 ka = kl[0], kb = kl[1];
         uint32_t a = c == 1u ? 0x3320646eu : c == 2u ? 0x79622d32u : 0x6b206574u;
         uint32_t bb = c == 1u ? ka.y : c == 2u ? ka.z : ka.w;
@@ -593,16 +613,21 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
           hc[0] = a; hc[1] = bb; hc[2] = cc; hc[3] = d;
         }
       }
-      {
+      if constexpr (G == 2) {  // no lanes 1..3 to hold the hoisted columns: the whole block
+        // (every lane computes a block, also one whose slot has no packet and whose record is stale: its key
+        // index is 0 then, and any index is clamped to the table)
+        const uint32_t kidx = have ? min(meta.w >> 8, P.key_slots - 1u) : 0u;
+        chacha20_block_full((const uint4*)(P.keys + 8u * kidx), b, meta.x, meta.y, 0u, x);
+      } else {
         const uint32_t H[12] = {bcastg<G, 1>(hc[0]), bcastg<G, 1>(hc[1]), bcastg<G, 1>(hc[2]), bcastg<G, 1>(hc[3]),
                                 bcastg<G, 2>(hc[0]), bcastg<G, 2>(hc[1]), bcastg<G, 2>(hc[2]), bcastg<G, 2>(hc[3]),
                                 bcastg<G, 3>(hc[0]), bcastg<G, 3>(hc[1]), bcastg<G, 3>(hc[2]), bcastg<G, 3>(hc[3])};
         if constexpr (!ST) {
-          chacha20_block_hoisted(rec[s].key, b, meta.x, meta.y, 0u, H, x);
+          chacha20_block_hoisted(RS(s).key, b, meta.x, meta.y, 0u, H, x);
         } else {
           // the same block in two parts: the first kStitchDR double rounds (with the pending Horner steps of the
           // previous round when any slot has them), then the payload DMA, then the rest and the feed-forward
-          const uint4* kl = rec[s].key;
+          const uint4* kl = RS(s).key;
           uint4 ka = kl[0], kb = kl[1];
           x[0] = 0x61707865u; x[1] = H[0]; x[2] = H[4]; x[3] = H[8];
           x[4] = ka.x; x[5] = H[1]; x[6] = H[5]; x[7] = H[9];
@@ -618,7 +643,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
             const uint32_t u = 4u * G * kp + ((j - ((4u * G * kp - 4u + Dp) & JM)) & JM);  // c0 + 4
             const uint32_t lanepart = ((u >> 2) - G * kp) & (G / 4u - 1u);
             const uint32_t addr = (uint32_t)(uintptr_t)&img[64u * (u & 3u) + (lane & ~JM) + lanepart];
-            const uint4 q0 = rec[s].R0, q1 = rec[s].R1, q2 = rec[s].R2;
+            const uint4 q0 = RS(s).R0, q1 = RS(s).R1, q2 = RS(s).R2;
             const uint32_t R[5] = {q0.x, q0.y, q0.z, q0.w, q1.x};
             const uint32_t Rs[4] = {q1.y, q1.z, q1.w, q2.x};
             // a lane whose first chunk of round 0's window lies before the data (u < 4: chunks -4..-1) adds it
@@ -645,8 +670,13 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
     if (__any(have && round == 0 && mac_pass)) {  // round 0: lane 0 of the slot holds the one-time key r || s
       const uint32_t lane = opaque_lane(), s = lane >> SH;
       if (have && round == 0 && mac_pass && (lane & JM) == 0) {
-        rec[s].R0 = make_uint4(x[0], x[1], x[2], x[3]);  // raw r, replaced by R = r^8 below
-        rec[s].s = make_uint4(x[4], x[5], x[6], x[7]);
+        RS(s).R0 = make_uint4(x[0], x[1], x[2], x[3]);  // raw r, replaced by R = r^8 below
+        if constexpr (G == 2) {
+          RS(s).R1 = make_uint4(0u, x[4], x[5], x[6]);
+          RS(s).R2.x = x[7];
+        } else {
+          RS(s).s = make_uint4(x[4], x[5], x[6], x[7]);
+        }
       }
     }
 
@@ -658,7 +688,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
       if (have && b < nb && b > 0u) {
         const uint32_t off = 64u * (b - 1u);
         const uint32_t nbytes = min(64u, len - off);
-        const uint4 ad = rec[s].addr;
+        const uint4 ad = RS(s).addr;
         uint8_t* dst = P.out + (((uint64_t)ad.z | ((uint64_t)ad.w << 32)) + off);
         const uint32_t oal = meta.w & 12u;  // bit 2: 16-B aligned output, bit 3: 4-B aligned
         // the payload DMA (and the staged loads) must have landed in LDS: the compiler does not
@@ -707,7 +737,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
     if (__any(have && round == 0 && mac_pass)) {
       if (have && round == 0 && mac_pass) {
         const uint32_t lane = opaque_lane(), s = lane >> SH, j = lane & JM;
-        const uint4 rr = rec[s].R0;
+        const uint4 rr = RS(s).R0;
         uint32_t y[5];
         poly_r_limbs(rr.x, rr.y, rr.z, rr.w, y);
 #pragma unroll
@@ -732,13 +762,17 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
           uint32_t Q[5] = {R[0], R[1], R[2], R[3], R[4]}, Rs[5];
           poly_scale5(R, Rs);
           poly_mul(Q, R, Rs);
-          rec[s].R0 = make_uint4(R[0], R[1], R[2], R[3]);
-          rec[s].R1 = make_uint4(R[4], Q[0], Q[1], Q[2]);
-          rec[s].R2 = make_uint4(Q[3], Q[4], 0u, 0u);
+          RS(s).R0 = make_uint4(R[0], R[1], R[2], R[3]);
+          RS(s).R1 = make_uint4(R[4], Q[0], Q[1], Q[2]);
+          RS(s).R2 = make_uint4(Q[3], Q[4], 0u, 0u);
 #else
-          rec[s].R0 = make_uint4(R[0], R[1], R[2], R[3]);
-          rec[s].R1 = make_uint4(R[4], 5u * R[1], 5u * R[2], 5u * R[3]);
-          rec[s].R2 = make_uint4(5u * R[4], 0u, 0u, 0u);
+          RS(s).R0 = make_uint4(R[0], R[1], R[2], R[3]);
+          if constexpr (G == 2) {
+            RS(s).R1.x = R[4];
+          } else {
+            RS(s).R1 = make_uint4(R[4], 5u * R[1], 5u * R[2], 5u * R[3]);
+            RS(s).R2 = make_uint4(5u * R[4], 0u, 0u, 0u);
+          }
 #endif
         }
       }
@@ -759,7 +793,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         const uint32_t c0 = c_lo + ((j - ((c_lo + D) & JM)) & JM);
         // chunk ci of the round sits in lane (ci >> 2) + 1 - G round of the slot, row ci & 3
         const uint4* ip = &img[64u * (c0 & 3u) + (lane & ~JM) + ((c0 + 4u) >> 2) - G * round];
-        const uint4 q0 = rec[s].R0, q1 = rec[s].R1, q2 = rec[s].R2;
+        const uint4 q0 = RS(s).R0, q1 = RS(s).R1, q2 = RS(s).R2;
 #ifdef WG_HORNER2
         // (opt-in, -DWG_HORNER2) two chunks per reduction where the round has them:
         // acc = acc R^2 + m_t R + m_(t+1). Bit-exact, but it spills 2 VGPRs in k_step<8> and ran
@@ -798,11 +832,14 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         }
 #else
         const uint32_t R[5] = {q0.x, q0.y, q0.z, q0.w, q1.x};
-        const uint32_t Rs[5] = {0u, q1.y, q1.z, q1.w, q2.x};
+        const uint32_t Rs[5] = {0u, G == 2 ? 5u * q0.y : q1.y, G == 2 ? 5u * q0.z : q1.z, G == 2 ? 5u * q0.w : q1.w,
+                                G == 2 ? 5u * q1.x : q2.x};
 #pragma unroll
         for (uint32_t t = 0; t < 4u; ++t) {
           if (c0 + G * t < c_end) {
-            uint4 v = ip[(G / 4u) * t];
+            // (2-lane slots: chunk c0 + 2 t alternates rows, so its place is computed per step)
+            uint4 v = G == 2 ? img[64u * ((c0 + 2u * t) & 3u) + (lane & ~JM) + ((c0 + 2u * t + 4u) >> 2) - G * round]
+                             : ip[(G / 4u) * t];
             // acc is still 0 before a packet's first chunk (round 0, t = 0): no product needed
             if (round != 0 || t != 0) poly_mul(acc, R, Rs);
             uint32_t cl[5];
@@ -825,13 +862,14 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         if (mac_pass) {
           if (valid) {
             if (j == JM && ((len + 15u) >> 4) >= 4u * G * round + 4u * G - 4u) {  // length block not taken in the loop
-              const uint4 q0 = rec[s].R0, q1 = rec[s].R1;
+              const uint4 q0 = RS(s).R0, q1 = RS(s).R1;
               const uint32_t R[5] = {q0.x, q0.y, q0.z, q0.w, q1.x};
 #ifdef WG_HORNER2
               const uint32_t Rs[5] = {0u, 5u * q0.y, 5u * q0.z, 5u * q0.w, 5u * q1.x};
 #else
-              const uint4 q2 = rec[s].R2;
-              const uint32_t Rs[5] = {0u, q1.y, q1.z, q1.w, q2.x};
+              const uint4 q2 = RS(s).R2;
+              const uint32_t Rs[5] = {0u, G == 2 ? 5u * q0.y : q1.y, G == 2 ? 5u * q0.z : q1.z,
+                                      G == 2 ? 5u * q0.w : q1.w, G == 2 ? 5u * q1.x : q2.x};
 #endif
               poly_mul(acc, R, Rs);
               acc[2] += (len << 12) & M26;  // le64(len) at bit 64: limb 2 holds bits 52..77
@@ -845,18 +883,18 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
 #pragma unroll
           for (int i = 0; i < 5; ++i) {  // slot sum (every lane of the slot ends with it)
             acc[i] += xor1_dpp(acc[i]);
-            acc[i] += xor2_dpp(acc[i]);
+            if constexpr (G >= 4) acc[i] += xor2_dpp(acc[i]);
             if constexpr (G >= 8) acc[i] += xor4_dpp(acc[i]);
             if constexpr (G == 16) acc[i] += xor8_dpp(acc[i]);
           }
         }
-        const uint4 ad = rec[s].addr;
+        const uint4 ad = RS(s).addr;
         const uint8_t* inp = P.in + ((uint64_t)ad.x | ((uint64_t)ad.y << 32));
         uint8_t* outp = P.out + ((uint64_t)ad.z | ((uint64_t)ad.w << 32));
         uint32_t bad = valid ? 0u : 1u;
         bool again = false;  // a verify-first open whose tag verified: the decrypt pass comes next
         if (mac_pass && valid && j == 0) {
-          const uint4 sv = rec[s].s;
+          const uint4 sv = G == 2 ? make_uint4(RS(s).R1.y, RS(s).R1.z, RS(s).R1.w, RS(s).R2.x) : RS(s).s;
           uint32_t tag[4];
           poly_finish(acc, sv.x, sv.y, sv.z, sv.w, tag);
           if constexpr (MODE == WG_MODE_SEAL) {
@@ -881,7 +919,7 @@ __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_
         }
         if constexpr (MODE == WG_MODE_OPEN) {
           if (again) {  // decrypt pass: the same rounds again, keystream XOR and stores only
-            if (j == 0) rec[s].meta.w = meta.w | kDecryptPass;
+            if (j == 0) RS(s).meta.w = meta.w | kDecryptPass;
             round = ~0u;  // incremented to 0 below
           } else {
             if (j == 0 && P.status) {
@@ -929,15 +967,20 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
 // resident): the hardware dispatcher starts each new workgroup as an old one retires, longest
 // packets first. Workgroups [0, b16) run the 16-lane body, [b16, b16 + b8) the 8-lane body; the
 // rest of the (host-sized, upper-bound) grid exits at once.
-template <int GS = 8>
+template <int GS = 8, int GT = 0>
 __device__ __forceinline__ int mixed_part(const TransportParams& P, uint32_t blk, TransportParams& Q, uint32_t& qblk) {
   Q = P;
-  uint32_t nl;
+  uint32_t nl, nt = 0;
   if (P.bin_cnt) {  // one-launch planning: the bins' counts, the long packets those of keys above the split
     nl = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < kFastBins; ++k) nl += k > P.split ? ((const WG_CONST uint32_t*)P.bin_cnt)[k] : 0u;
+    for (uint32_t k = 0; k < kFastBins; ++k) {
+      const uint32_t c = ((const WG_CONST uint32_t*)P.bin_cnt)[k];
+      nl += k > P.split ? c : 0u;
+      if constexpr (GT != 0) nt += k <= P.split2 ? c : 0u;  // (split2 = 0: only key 0, the invalid packets)
+    }
     nl = min(nl, P.n);
+    if constexpr (GT != 0) nt = P.split2 ? min(nt, P.n - nl) : 0u;
   } else {
     nl = min(__builtin_amdgcn_readfirstlane(*(const WG_CONST uint32_t*)P.n_long), P.n);
   }
@@ -949,14 +992,27 @@ __device__ __forceinline__ int mixed_part(const TransportParams& P, uint32_t blk
     return 16;
   }
   constexpr uint32_t spw = 64u / GS;  // short slots per wave
-  const uint32_t ns = P.n - nl, bs = (ns + spw * TW - 1u) / (spw * TW);
-  if (blk - b16 >= bs) return 0;
-  if (P.bin_cnt) Q.pos_base = nl;  // the sparse order's positions run on past the long packets
-  else Q.order = P.order + nl;
-  Q.n = ns;
-  Q.slots = bs * TW * spw;
-  qblk = blk - b16;
-  return GS;
+  const uint32_t ns = P.n - nl - nt, bs = (ns + spw * TW - 1u) / (spw * TW);
+  if (blk - b16 < bs) {
+    if (P.bin_cnt) Q.pos_base = nl;  // the sparse order's positions run on past the long packets
+    else Q.order = P.order + nl;
+    Q.n = ns;
+    Q.slots = bs * TW * spw;
+    qblk = blk - b16;
+    return GS;
+  }
+  if constexpr (GT != 0) {  // the tiny packets (keys <= split2, at the end of the order) in GT-lane slots
+    constexpr uint32_t tpw = 64u / GT;
+    const uint32_t bt = (nt + tpw * TW - 1u) / (tpw * TW);
+    if (blk - b16 - bs < bt) {
+      Q.pos_base = nl + ns;
+      Q.n = nt;
+      Q.slots = bt * TW * tpw;
+      qblk = blk - b16 - bs;
+      return GT;
+    }
+  }
+  return 0;
 }
 
 template <int MODE, bool VF = false, int GS = 8>
@@ -974,24 +1030,35 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
 #ifndef WG_STITCH_WPE
 #define WG_STITCH_WPE 5  // waves per SIMD the stitched kernels' register allocation targets (96 VGPRs: no spill)
 #endif
-template <int GS = 8, bool ST = false>
+// GT = 2: a third part after the GS-lane one, the tiny packets (keys <= split2) in 2-lane slots (32 per wave:
+// a 40-B packet's two blocks fill its lanes instead of half of a 4-lane slot). Its records need twice the LDS.
+template <int GS = 8, bool ST = false, int GT = 0>
 __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(ST ? WG_STITCH_WPE : 8)))
 k_step_mixed(TransportParams S, TransportParams O) {
   __shared__ uint4 img_[TW][4 * 64];
-  __shared__ SlotRec rec_[TW][64 / GS];
+  // slot records: 128 B per GS- or 16-lane slot, 80 B per 2-lane slot (transport_body's kRecStride)
+  constexpr uint32_t kRecU4 = GT ? ((64 / GS) * 8 > (64 / GT) * 5 ? (64 / GS) * 8 : (64 / GT) * 5) : (64 / GS) * 8;
+  __shared__ uint4 recraw_[TW][kRecU4];
+  SlotRec* const rec = (SlotRec*)recraw_[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   TransportParams QS, QO;
   uint32_t qb = 0, qb2 = 0, iter = 0;
-  const int g = mixed_part<GS>(S, blockIdx.x, QS, qb);
-  (void)mixed_part<GS>(O, blockIdx.x, QO, qb2);  // the same split: the open batch has the seal's lengths
+  const int g = mixed_part<GS, GT>(S, blockIdx.x, QS, qb);
+  (void)mixed_part<GS, GT>(O, blockIdx.x, QO, qb2);  // the same split: the open batch has the seal's lengths
   if (g == 16) {
-    transport_body<WG_MODE_SEAL, 16, false, kPosStatic, ST, true>(QS, qb, wv, img_[wv], rec_[wv], iter);
+    transport_body<WG_MODE_SEAL, 16, false, kPosStatic, ST, true>(QS, qb, wv, img_[wv], rec, iter);
     asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
-    transport_body<WG_MODE_OPEN, 16, false, kPosStatic, ST, true>(QO, qb, wv, img_[wv], rec_[wv], iter);
+    transport_body<WG_MODE_OPEN, 16, false, kPosStatic, ST, true>(QO, qb, wv, img_[wv], rec, iter);
   } else if (g == GS) {
-    transport_body<WG_MODE_SEAL, GS, false, kPosStatic, ST, true>(QS, qb, wv, img_[wv], rec_[wv], iter);
+    transport_body<WG_MODE_SEAL, GS, false, kPosStatic, ST, true>(QS, qb, wv, img_[wv], rec, iter);
     asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
-    transport_body<WG_MODE_OPEN, GS, false, kPosStatic, ST, true>(QO, qb, wv, img_[wv], rec_[wv], iter);
+    transport_body<WG_MODE_OPEN, GS, false, kPosStatic, ST, true>(QO, qb, wv, img_[wv], rec, iter);
+  } else if constexpr (GT != 0) {
+    if (g == GT) {
+      transport_body<WG_MODE_SEAL, GT, false, kPosStatic, false, true>(QS, qb, wv, img_[wv], rec, iter);
+      asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
+      transport_body<WG_MODE_OPEN, GT, false, kPosStatic, false, true>(QO, qb, wv, img_[wv], rec, iter);
+    }
   }
 }
 
