@@ -111,3 +111,13 @@ def test_bench_imix_fused_planning_is_verified():
                 {"WG_LPT_FUSED": "1", "WG_FUSED_POLL": "1", "WG_FUSED_NP": "7"}):
         rc, line = _bench(env, "3", "--workload", "imix")
         assert rc == 0 and line["verified"] is True and line["oracle_sample"]["bit_exact"] is True, (env, line)
+
+
+def test_bench_imix_two_streams_own_workspaces():
+    """IMIX on two streams (--streams 2): each stream's k_lpt_one plans into its own workspace (WG_STREAM_WS,
+    on by default), so the halves run concurrently; with WG_STREAM_WS=0 they share one workspace and wait for
+    each other. Every packet of both halves must round-trip and the oracle sample be bit-exact either way."""
+    for env in ({}, {"WG_STREAM_WS": "0"}):
+        rc, line = _bench(env, "3", "--workload", "imix", "--streams", "2")
+        assert rc == 0 and line["verified"] is True and line["oracle_sample"]["bit_exact"] is True, (env, line)
+        assert line["config"]["streams"] == 2

@@ -153,6 +153,19 @@ struct wg_ctx {
   DevBuf lpt_hist2, lpt_order2;  // the open half of a wg_duplex_batch
   DevBuf lpt_nlong;              // k_lpt_scatter -> k_*_mixed: long packets at the front of lpt_order
   DevBuf lpt_claim, lpt_chain;   // k_step_claim: sub-order counters (64-B lines) and the seal half's per-position log
+  // per-stream plan workspaces for the short-packet split plan's WG_F_AFTER_SEAL steps (k_lpt_one's counters
+  // and sparse order): calls on different streams then plan and run concurrently instead of waiting for
+  // each other's workspace (ws_acquire). Up to kStreamWS streams; each use waits for the workspace's last
+  // use (an event: a no-op on its own stream, an order if a stream handle was reused). WG_STREAM_WS=0: off
+  struct StreamWS {
+    hipStream_t s = nullptr;
+    DevBuf hist, order;
+    hipEvent_t ev = nullptr;
+    bool used = false;
+  };
+  static constexpr size_t kStreamWS = 8;
+  std::vector<std::unique_ptr<StreamWS>> stream_ws;
+  bool stream_ws_on = true;
 
   int kern = KERN_TRANSPORT;
   // host-API staging
@@ -672,6 +685,18 @@ hipStream_t pick_stream(wg_ctx*, void* stream) { return (hipStream_t)stream; }
 // wrote, on `s`. A mixed-length batch is ordered longest-first once: the open's packets have the
 // seal's lengths, so it reuses the seal's order (one k_lpt_* pair per step instead of two). The
 // plan workspace is held from the seal's order to the open. Caller holds c->mu.
+// The stream's own plan workspace (created on first use), or nullptr when kStreamWS streams have one already.
+wg_ctx::StreamWS* stream_ws(wg_ctx* c, hipStream_t s) {
+  for (auto& w : c->stream_ws)
+    if (w->s == s) return w.get();
+  if (c->stream_ws.size() >= wg_ctx::kStreamWS) return nullptr;
+  auto w = std::make_unique<wg_ctx::StreamWS>();
+  w->s = s;
+  if (hipEventCreateWithFlags(&w->ev, hipEventDisableTiming) != hipSuccess) return nullptr;
+  c->stream_ws.push_back(std::move(w));
+  return c->stream_ws.back().get();
+}
+
 int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStream_t s) {
   const bool same_plan = sb->max_len == ob->max_len && (sb->flags & WG_F_UNIFORM) == (ob->flags & WG_F_UNIFORM) &&
                          c->resident_waves[0][0] == c->resident_waves[0][1] &&
@@ -694,7 +719,16 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
     }
   }
   int rc;
-  if (ordered && (rc = ws_acquire(c, s)) != WG_OK) return rc;
+  // the short-packet split plan in one launch (plan_transport's `one`) on the stream's own workspace
+  wg_ctx::StreamWS* pws = nullptr;
+  if (fused && c->stream_ws_on && !(sb->flags & WG_F_UNIFORM) && sb->max_len <= 2048u && c->lpt_one &&
+      !(c->lpt_fused && !c->stitch) && slot_plan(c, sb->flags, sb->n, sb->max_len).split > 0) {
+    pws = stream_ws(c, s);
+    if (pws && pws->used) HIPTRY(hipStreamWaitEvent(s, pws->ev, 0));
+  }
+  DevBuf& plan_hist = pws ? pws->hist : c->lpt_hist;
+  DevBuf& plan_order = pws ? pws->order : c->lpt_order;
+  if (ordered && !pws && (rc = ws_acquire(c, s)) != WG_OK) return rc;
   if (fused) {
     const SlotPlan sp = slot_plan(c, sb->flags, sb->n, sb->max_len);
     const uint32_t G = sp.G;
@@ -722,13 +756,13 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
         c->lpt_claim.ensure(64u * 64u) == WG_OK && c->lpt_chain.ensure(sizeof(uint2) * (size_t)sb->n) == WG_OK)
       claim_nc = 64;
     rc = plan_transport<WG_MODE_SEAL>(c, sb->desc, sb->n, sb->in, sb->in_size, sb->out, sb->out_size, nullptr,
-                                      sb->max_len, sb->flags, s, cap, G, c->lpt_hist, c->lpt_order, &PS, &gs, &os,
+                                      sb->max_len, sb->flags, s, cap, G, plan_hist, plan_order, &PS, &gs, &os,
                                       nullptr, true, false, sp.split, claim_nc ? (uint32_t*)c->lpt_claim.p : nullptr,
                                       claim_nc, &defer);
     if (rc == WG_OK)
       rc = plan_transport<WG_MODE_OPEN>(c, ob->desc, ob->n, ob->in, ob->in_size, ob->out, ob->out_size, ob->status,
-                                        ob->max_len, ob->flags & ~WG_F_AFTER_SEAL, s, cap, G, c->lpt_hist,
-                                        c->lpt_order, &PO, &go, &oo, nullptr, true, true, sp.split);
+                                        ob->max_len, ob->flags & ~WG_F_AFTER_SEAL, s, cap, G, plan_hist,
+                                        plan_order, &PO, &go, &oo, nullptr, true, true, sp.split);
     // one issue-priority schedule over the seal and open halves (the rounds of both)
     if (PS.prio_step) PS.prio_step = PO.prio_step = 2u * PS.prio_step;
     if (claim_nc) {
@@ -795,6 +829,11 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
       rc = launch_transport<WG_MODE_OPEN>(c, ob->desc, ob->n, ob->in, ob->in_size, ob->out, ob->out_size, ob->status,
                                           ob->max_len, ob->flags & ~WG_F_AFTER_SEAL, s, nullptr, &c->lpt_hist,
                                           &c->lpt_order, same_plan);
+  }
+  if (pws) {  // the workspace's last use, for the next call that takes it
+    if (hipEventRecord(pws->ev, s) != hipSuccess) return fail(WG_EDEVICE, "hipEventRecord failed");
+    pws->used = true;
+    return rc;
   }
   const int rr = ordered ? ws_release(c, s) : WG_OK;
   return rc != WG_OK ? rc : rr;
@@ -904,6 +943,7 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   if (const char* e = getenv("WG_LPT_ONE")) c->lpt_one = atoi(e) != 0;
   if (const char* e = getenv("WG_LPT_FUSED")) c->lpt_fused = atoi(e) != 0;
   if (const char* e = getenv("WG_SLOT2")) c->slot2 = (uint32_t)std::max(0, atoi(e));
+  if (const char* e = getenv("WG_STREAM_WS")) c->stream_ws_on = atoi(e) != 0;
   if (const char* e = getenv("WG_FUSED_POLL")) c->fused_poll = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_FUSED_NP")) c->fused_np = (uint32_t)std::max(0, atoi(e));
 #ifdef WG_TEST_HOOKS
@@ -942,6 +982,11 @@ int wg_ctx_destroy(wg_ctx* c) {
                     &c->h_keys})
     b->release();
   if (c->plan_err) (void)hipHostFree(c->plan_err);
+  for (auto& w : c->stream_ws) {
+    w->hist.release();
+    w->order.release();
+    if (w->ev) (void)hipEventDestroy(w->ev);
+  }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->copy_out_stream) (void)hipStreamDestroy(c->copy_out_stream);
