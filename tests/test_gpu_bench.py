@@ -121,3 +121,11 @@ def test_bench_imix_two_streams_own_workspaces():
         rc, line = _bench(env, "3", "--workload", "imix", "--streams", "2")
         assert rc == 0 and line["verified"] is True and line["oracle_sample"]["bit_exact"] is True, (env, line)
         assert line["config"]["streams"] == 2
+
+
+def test_bench_imix_graph_is_verified():
+    """IMIX captured into a HIP graph (--graph): the capture stream has no plan workspace of its own and cannot
+    allocate one, so it plans in the shared workspace the earlier calls sized; every packet must round-trip."""
+    rc, line = _bench({}, "3", "--workload", "imix", "--graph")
+    assert rc == 0 and line["verified"] is True and line["oracle_sample"]["bit_exact"] is True, line
+    assert line["graph"] is True

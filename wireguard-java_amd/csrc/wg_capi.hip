@@ -690,6 +690,9 @@ wg_ctx::StreamWS* stream_ws(wg_ctx* c, hipStream_t s) {
   for (auto& w : c->stream_ws)
     if (w->s == s) return w.get();
   if (c->stream_ws.size() >= wg_ctx::kStreamWS) return nullptr;
+  // a stream being captured into a graph cannot allocate: it takes the shared workspace, as before
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
   auto w = std::make_unique<wg_ctx::StreamWS>();
   w->s = s;
   if (hipEventCreateWithFlags(&w->ev, hipEventDisableTiming) != hipSuccess) return nullptr;
@@ -725,6 +728,11 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
       !(c->lpt_fused && !c->stitch) && slot_plan(c, sb->flags, sb->n, sb->max_len).split > 0) {
     pws = stream_ws(c, s);
     if (pws && pws->used) HIPTRY(hipStreamWaitEvent(s, pws->ev, 0));
+    // the shared workspace sized too: a later call on a stream being captured into a graph (no workspace of
+    // its own, and no allocation possible) plans there
+    if (pws && (c->lpt_hist.ensure(2 * wgt::kPlanSet * sizeof(uint32_t)) != WG_OK ||
+                c->lpt_order.ensure(sizeof(uint32_t) * wgt::kFastBins * (size_t)sb->n) != WG_OK))
+      return WG_ENOMEM;
   }
   DevBuf& plan_hist = pws ? pws->hist : c->lpt_hist;
   DevBuf& plan_order = pws ? pws->order : c->lpt_order;
