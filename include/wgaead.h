@@ -201,7 +201,9 @@ int wg_open_batch(wg_ctx* ctx, const wg_pkt* desc_dev, uint32_t n, const uint8_t
  *   equal max_len / WG_F_UNIFORM on both sides (and no WG_F_FRAME) the step is ONE k_step launch in
  *   which every wave seals its packets and then opens the same batch positions; otherwise the seal
  *   launch and then the open launch run on `stream`. A mixed-length batch is ordered longest-first
- *   once, for both (its packets have the same lengths). */
+ *   once, for both (its packets have the same lengths). Such a step on a mixed batch of max_len <= 2048
+ *   plans in a workspace of its stream's own (up to 8 streams; WG_STREAM_WS=0: the shared one), so steps
+ *   on different streams do not wait for each other. */
 #define WG_F_AFTER_SEAL 4u
 typedef struct wg_batch {
   const wg_pkt* desc; /* device, 16-byte aligned */
