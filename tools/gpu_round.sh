@@ -47,6 +47,8 @@ cat $O/bench_c2.json
 step "bench imix"
 timeout -k 10 300 python bench.py --workload imix > $O/bench_imix.json 2>> $O/bench.err || die bench_imix $?
 cat $O/bench_imix.json
+timeout -k 10 300 python bench.py --workload imix --graph --no-cpu-baseline > $O/bench_imix_graph.json 2>> $O/bench.err || die bench_imix_graph $?
+cat $O/bench_imix_graph.json
 step "bench c3"
 timeout -k 10 400 python bench.py --workload c3 --no-cpu-baseline --steps 5 --warmup 1 > $O/bench_c3.json 2>> $O/bench.err || die bench_c3 $?
 cat $O/bench_c3.json
