@@ -84,6 +84,15 @@ def trace(args):
                         "max_us": round(max(v), 3), "median_us": round(sorted(v)[len(v) // 2], 3)}
                     for k, v in sorted(per_kernel.items())},
     }
+    # the step's other launches inside the window (the mixed plans' k_lpt_* planning): the device time a
+    # step needs besides the transport kernel, so that the gaps left are the host's
+    t0, t1 = int(win[0]["Start_Timestamp"]), int(win[-1]["End_Timestamp"])
+    plan_us = sum((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3
+                  for r in csv.DictReader(open(args.csv)) if re.search(r"k_lpt_", r["Kernel_Name"])
+                  and t0 <= int(r["Start_Timestamp"]) and int(r["End_Timestamp"]) <= t1)
+    if plan_us:
+        out["planning_busy_per_step_us"] = round(plan_us / b["steps"], 3)
+        out["gap_per_step_us"] = round((span_us - busy_us - plan_us) / b["steps"], 3)
     st = b["roofline"].get("step") or {}
     multi = st.get("streams", 1) > 1
     # per step: a K-stream step's K launches together move one batch (the one-stream kernel's bytes)
@@ -103,7 +112,7 @@ def trace(args):
     out["frac_from_kernel_time"] = round(alg / (busy_us / b["steps"] * 1e-6) / 8.0e12, 4)
     # K streams overlap their launches: the summed durations exceed the span, so only the span says
     # whether the host kept the device fed
-    out["host_bound_under_profiler"] = span_us > 1.05 * busy_us if not multi else \
+    out["host_bound_under_profiler"] = span_us > 1.05 * (busy_us + plan_us) if not multi else \
         span_us / b["steps"] * 1e-3 > 1.05 * b["ms_per_step"]
     return out
 

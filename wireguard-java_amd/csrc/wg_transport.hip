@@ -322,6 +322,13 @@ __device__ __forceinline__ uint32_t batch_pos(uint32_t g, uint32_t k, uint32_t S
 // batch position -> packet index: the identity, the dense longest-first order, or the sparse one of k_lpt_one
 // (keys descending, key k's packets at order[k * bin_cap + i])
 constexpr uint32_t kFastBins = 6;  // keys 0..5: every packet of at most 2,048 B (33 blocks, 5 rounds of 8)
+// k_lpt_one's per-key counters, kCntStride words apart (every planner workgroup adds to each once). 16 (a
+// 64-B line each) measured the same as 1: the planner's 5.1 us is not atomic contention
+// (profiles/r06_cnt_stride_ab.jsonl)
+#ifndef WG_CNT_STRIDE
+#define WG_CNT_STRIDE 1
+#endif
+constexpr uint32_t kCntStride = WG_CNT_STRIDE;
 template <bool MX>
 __device__ __forceinline__ uint32_t pkt_at(const TransportParams& P, uint32_t pos) {
   if (MX && P.bin_cap) {
@@ -332,7 +339,7 @@ __device__ __forceinline__ uint32_t pkt_at(const TransportParams& P, uint32_t po
     uint32_t start = 0, at = 0;
 #pragma unroll
     for (int k = (int)kFastBins - 1; k >= 0; --k) {
-      const uint32_t c = bc[k];
+      const uint32_t c = bc[k * kCntStride];
       at = (p >= start) ? (uint32_t)k * P.bin_cap + (p - start) : at;
       start += c;
     }
@@ -975,7 +982,7 @@ __device__ __forceinline__ int mixed_part(const TransportParams& P, uint32_t blk
     nl = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kFastBins; ++k) {
-      const uint32_t c = ((const WG_CONST uint32_t*)P.bin_cnt)[k];
+      const uint32_t c = ((const WG_CONST uint32_t*)P.bin_cnt)[k * kCntStride];
       nl += k > P.split ? c : 0u;
       if constexpr (GT != 0) nt += k <= P.split2 ? c : 0u;  // (split2 = 0: only key 0, the invalid packets)
     }
@@ -1250,9 +1257,10 @@ __global__ void __launch_bounds__(LPT_THREADS) k_lpt_scatter(const wg_pkt* d, ui
   for (uint32_t i = lo + threadIdx.x; i < hi; i += LPT_THREADS) order[atomicAdd(&base[lpt_key<MODE>(d, i, max_len)], 1u)] = i;
 }
 
-// k_lpt_one's counter set: 64 words per call (counts at [0, kFastBins), the fused step's publication count at
+// k_lpt_one's counter set per call: the counts kCntStride words apart, the fused step's publication count at
 // kPlanDone), two sets used in turn
-constexpr uint32_t kPlanSet = 64, kPlanDone = 32;
+constexpr uint32_t kPlanDone = kFastBins * kCntStride > 32u ? kFastBins * kCntStride : 32u;
+constexpr uint32_t kPlanSet = kPlanDone + 32u;  // words per set (the publication count on a line of its own)
 
 // The body of k_lpt_one for block `blk` of `nblk` with `threads` threads: h / base are kFastBins words of LDS.
 // A thread takes KPT packets per trip, their descriptor loads issued together, and when the block's range is
@@ -1264,7 +1272,8 @@ __device__ __forceinline__ void lpt_one_body(const wg_pkt* d, uint32_t n, uint32
   if (threadIdx.x < kFastBins) h[threadIdx.x] = 0;
   // the next call's counts ([0, kFastBins)) and k_step_mixed_fused's publication count (kPlanDone: its own line,
   // away from the counts' atomics)
-  if (blk == 0 && (threadIdx.x < 8u || threadIdx.x == kPlanDone)) cnt_next[threadIdx.x] = 0;
+  if (blk == 0 && ((threadIdx.x < kFastBins * kCntStride && threadIdx.x % kCntStride == 0u) || threadIdx.x == kPlanDone))
+    cnt_next[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t per = (n + nblk - 1u) / nblk;
   const uint32_t lo = min(n, blk * per), hi = min(n, lo + per);
@@ -1301,7 +1310,7 @@ __device__ __forceinline__ void lpt_one_body(const wg_pkt* d, uint32_t n, uint32
   __syncthreads();
   if (threadIdx.x < kFastBins) {
     const uint32_t k = threadIdx.x, c = h[k];
-    base[k] = k * n + (c ? atomicAdd(&cnt[k], c) : 0u);
+    base[k] = k * n + (c ? atomicAdd(&cnt[k * kCntStride], c) : 0u);
   }
   __syncthreads();
   const bool one_trip = hi - lo <= span;
