@@ -501,6 +501,8 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
       if (may_defer) {  // the caller's k_step_mixed_fused launch plans (into cnt / nxt, as below)
         *defer_one = true;
       } else {
+        // (block shapes of 256 / 512 threads or 4 packets per thread measured the same or slower: 5.0-8.3 us,
+        // profiles/r06_lpt_shape_ab.jsonl)
         hipLaunchKernelGGL((wgt::k_lpt_one<MODE>), dim3(lgrid), dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len, cnt,
                            nxt, (uint32_t*)lpt_order.p);
         HIPTRY(hipGetLastError());

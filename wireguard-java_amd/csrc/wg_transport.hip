@@ -1278,21 +1278,22 @@ __device__ __forceinline__ void lpt_one_body(const wg_pkt* d, uint32_t n, uint32
   const uint32_t per = (n + nblk - 1u) / nblk;
   const uint32_t lo = min(n, blk * per), hi = min(n, lo + per);
   const uint32_t lane = threadIdx.x & 63u, span = threads * KPT;
-  // LDS atomics are aggregated per wave and key (a ballot, one atomicAdd by the wave's first lane, ranks by
-  // mbcnt): a few keys shared by all threads would otherwise serialise on their LDS words
+  // LDS atomics are aggregated per wave and key: one ballot per key, then ONE ds_add_rtn in which lane k adds
+  // key k's lane count to slots[k] (six independent adds, not a chain of six round trips), one bpermute for
+  // each lane's base in its key and mbcnt for its rank among the wave's lanes of that key
   auto wave_rank = [&](uint32_t* slots, uint32_t key) {  // this lane's rank among the wave's lanes of its key
-    uint32_t r = 0;
+    uint64_t mine = 0;
+    uint32_t cnt_k = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kFastBins; ++k) {
       const uint64_t m = __ballot(key == k);
-      if (m) {
-        uint32_t b = 0;
-        if (lane == (uint32_t)__builtin_ctzll(m)) b = atomicAdd(&slots[k], (uint32_t)__popcll(m));
-        b = __shfl(b, (int)__builtin_ctzll(m), 64);
-        if (key == k) r = b + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-      }
+      mine = key == k ? m : mine;
+      cnt_k = lane == k ? (uint32_t)__popcll(m) : cnt_k;
     }
-    return r;
+    uint32_t b = 0;
+    if (cnt_k) b = atomicAdd(&slots[lane], cnt_k);  // lanes 0..kFastBins-1 only (cnt_k = 0 elsewhere)
+    b = __shfl(b, (int)(key < kFastBins ? key : 0u), 64);
+    return b + (uint32_t)__popcll(mine & ((1ull << lane) - 1ull));
   };
   auto keys_at = [&](uint32_t i0, uint32_t (&key)[KPT]) {  // every lane of a wave takes part in each trip
 #pragma unroll
@@ -1331,11 +1332,12 @@ __device__ __forceinline__ void lpt_one_body(const wg_pkt* d, uint32_t n, uint32
 // order (key k at order[k * n]). No grid-wide barrier: the consumer derives the positions from the counts.
 // The counters are double-buffered by call (cnt for this call, zero on entry; cnt_next zeroed here for the
 // next), so no memset launch either. Order inside a key: arbitrary (every position of the order is a packet).
-template <int MODE>
-__global__ void __launch_bounds__(LPT_THREADS) k_lpt_one(const wg_pkt* d, uint32_t n, uint32_t max_len, uint32_t* cnt,
-                                                         uint32_t* cnt_next, uint32_t* order) {
+// (THREADS, KPT: the block shape)
+template <int MODE, uint32_t THREADS = LPT_THREADS, int KPT = 1>
+__global__ void __launch_bounds__(THREADS) k_lpt_one(const wg_pkt* d, uint32_t n, uint32_t max_len, uint32_t* cnt,
+                                                     uint32_t* cnt_next, uint32_t* order) {
   __shared__ uint32_t h[kFastBins], base[kFastBins];
-  lpt_one_body<MODE>(d, n, max_len, cnt, cnt_next, order, blockIdx.x, gridDim.x, LPT_THREADS, h, base);
+  lpt_one_body<MODE, KPT>(d, n, max_len, cnt, cnt_next, order, blockIdx.x, gridDim.x, THREADS, h, base);
 }
 
 // k_step_mixed with its planning folded in (WG_LPT_FUSED, the short-packet plan): workgroups [0, np) plan as
