@@ -689,12 +689,13 @@ hipStream_t pick_stream(wg_ctx*, void* stream) { return (hipStream_t)stream; }
 // plan workspace is held from the seal's order to the open. Caller holds c->mu.
 // The stream's own plan workspace (created on first use), or nullptr when kStreamWS streams have one already.
 wg_ctx::StreamWS* stream_ws(wg_ctx* c, hipStream_t s) {
+  // a stream being captured into a graph takes the shared workspace, as before: it cannot allocate one, and
+  // its workspace's event would be recorded inside the graph
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
   for (auto& w : c->stream_ws)
     if (w->s == s) return w.get();
   if (c->stream_ws.size() >= wg_ctx::kStreamWS) return nullptr;
-  // a stream being captured into a graph cannot allocate: it takes the shared workspace, as before
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
   auto w = std::make_unique<wg_ctx::StreamWS>();
   w->s = s;
   if (hipEventCreateWithFlags(&w->ev, hipEventDisableTiming) != hipSuccess) return nullptr;
