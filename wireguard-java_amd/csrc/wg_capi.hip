@@ -155,15 +155,13 @@ struct wg_ctx {
   DevBuf lpt_claim, lpt_chain;   // k_step_claim: sub-order counters (64-B lines) and the seal half's per-position log
   // per-stream plan workspaces for the short-packet split plan's WG_F_AFTER_SEAL steps (k_lpt_one's counters
   // and sparse order): calls on different streams then plan and run concurrently instead of waiting for
-  // each other's workspace (ws_acquire). Up to kStreamWS streams. A workspace is only ever used by its own
-  // stream, so stream order protects it and no event is recorded per call (an event record after every step
-  // cost IMIX 6%: 722-739 against 774-777 GiB/s, profiles/r06_ws_event_ab.jsonl); a stream handle that a
-  // new stream reuses (a different hipStreamGetId) waits for the device once before taking the workspace
-  // over, since the destroyed stream's launches may still be running. WG_STREAM_WS=0: off
+  // each other's workspace (ws_acquire). Up to kStreamWS streams; each use waits for the workspace's last
+  // use (an event: a no-op on its own stream, an order if a stream handle was reused). WG_STREAM_WS=0: off
   struct StreamWS {
     hipStream_t s = nullptr;
-    unsigned long long id = 0;
     DevBuf hist, order;
+    hipEvent_t ev = nullptr;
+    bool used = false;
   };
   static constexpr size_t kStreamWS = 8;
   std::vector<std::unique_ptr<StreamWS>> stream_ws;
@@ -695,20 +693,12 @@ wg_ctx::StreamWS* stream_ws(wg_ctx* c, hipStream_t s) {
   // its workspace's event would be recorded inside the graph
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-  unsigned long long id = 0;
-  if (hipStreamGetId(s, &id) != hipSuccess) id = 0;
   for (auto& w : c->stream_ws)
-    if (w->s == s) {
-      if (w->id != id) {  // a new stream behind a reused handle: the old one's launches may still run
-        if (hipDeviceSynchronize() != hipSuccess) return nullptr;
-        w->id = id;
-      }
-      return w.get();
-    }
+    if (w->s == s) return w.get();
   if (c->stream_ws.size() >= wg_ctx::kStreamWS) return nullptr;
   auto w = std::make_unique<wg_ctx::StreamWS>();
   w->s = s;
-  w->id = id;
+  if (hipEventCreateWithFlags(&w->ev, hipEventDisableTiming) != hipSuccess) return nullptr;
   c->stream_ws.push_back(std::move(w));
   return c->stream_ws.back().get();
 }
@@ -740,6 +730,7 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
   if (fused && c->stream_ws_on && !(sb->flags & WG_F_UNIFORM) && sb->max_len <= 2048u && c->lpt_one &&
       !(c->lpt_fused && !c->stitch) && slot_plan(c, sb->flags, sb->n, sb->max_len).split > 0) {
     pws = stream_ws(c, s);
+    if (pws && pws->used) HIPTRY(hipStreamWaitEvent(s, pws->ev, 0));
     // the shared workspace sized too: a later call on a stream being captured into a graph (no workspace of
     // its own, and no allocation possible) plans there
     if (pws && (c->lpt_hist.ensure(2 * wgt::kPlanSet * sizeof(uint32_t)) != WG_OK ||
@@ -850,7 +841,11 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
                                           ob->max_len, ob->flags & ~WG_F_AFTER_SEAL, s, nullptr, &c->lpt_hist,
                                           &c->lpt_order, same_plan);
   }
-  if (pws) return rc;  // (stream order protects the stream's own workspace)
+  if (pws) {  // the workspace's last use, for the next call that takes it
+    if (hipEventRecord(pws->ev, s) != hipSuccess) return fail(WG_EDEVICE, "hipEventRecord failed");
+    pws->used = true;
+    return rc;
+  }
   const int rr = ordered ? ws_release(c, s) : WG_OK;
   return rc != WG_OK ? rc : rr;
 }
@@ -1001,6 +996,7 @@ int wg_ctx_destroy(wg_ctx* c) {
   for (auto& w : c->stream_ws) {
     w->hist.release();
     w->order.release();
+    if (w->ev) (void)hipEventDestroy(w->ev);
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
