@@ -482,3 +482,53 @@ def test_two_lane_slots_every_packet(slot2, workload):
             assert np.array_equal(back.cpu().numpy(), want)
     finally:
         eng.close()
+
+
+def test_short_plan_steps_on_destroyed_and_recreated_streams():
+    """Per-stream plan workspaces (WG_STREAM_WS) are keyed by stream handle; each use waits for the workspace's
+    last use (an event, WG_WSEV=3). A step on a stream that is destroyed while its launches run, then a step on
+    a new stream (which may get the same handle) with a DIFFERENT batch, must not plan into the workspace the
+    first step's kernel is still reading. Four rounds of create / step / destroy, each with its own
+    0..2,048-B batch, then every output against the oracle."""
+    import ctypes
+    torch, dev = _dev()
+    W = wg()
+    hip = ctypes.CDLL("libamdhip64.so")
+    eng = W.Engine(0, key_slots=256)
+    keys = splitmix_np(0x57EA, 32 * 256)
+    eng.set_keys(0, keys.tobytes())
+    runs = []
+    try:
+        for r in range(4):
+            n = 65536
+            lengths = (splitmix_np(0x5700 + r, 4 * n).view("<u4") % 2049).astype(np.int64)
+            S = ((lengths + 16 + 15) // 16) * 16
+            off = np.concatenate([[0], np.cumsum(S)[:-1]]).astype(np.uint64)
+            desc = W.pack_desc(off, off, np.arange(n, dtype=np.uint64) // 256, lengths, np.arange(n) % 256)
+            total = int(S.sum())
+            pt = splitmix_np(0x5701 + r, total)
+            d = torch.from_numpy(W.desc_as_int64(desc)).to(dev)
+            dpt = torch.from_numpy(pt).to(dev)
+            dct = torch.zeros(total, dtype=torch.uint8, device=dev)
+            back = torch.zeros(total, dtype=torch.uint8, device=dev)
+            st = torch.full((n,), 7, dtype=torch.int32, device=dev)
+            torch.cuda.synchronize()
+            s = ctypes.c_void_p()
+            assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+            step = eng.prepare_duplex(d, dpt, dct, 2048, d, dct, back, st, 2048, uniform=False, after_seal=True,
+                                      stream=s.value)
+            step()
+            assert hip.hipStreamDestroy(s) == 0  # while the step may still run
+            runs.append((lengths, S, off, total, desc, pt, d, dpt, dct, back, st))
+        torch.cuda.synchronize()
+        for lengths, S, off, total, desc, pt, d, dpt, dct, back, st in runs:
+            ref = np.zeros(total, np.uint8)
+            O.seal_batch(desc, pt, ref, keys, threads=16)
+            assert np.array_equal(dct.cpu().numpy(), ref)
+            assert int(st.abs().sum().item()) == 0
+            want = pt.copy()
+            for i in range(len(lengths)):
+                want[int(off[i]) + int(lengths[i]):int(off[i]) + int(S[i])] = 0
+            assert np.array_equal(back.cpu().numpy(), want)
+    finally:
+        eng.close()

@@ -166,6 +166,7 @@ struct wg_ctx {
   static constexpr size_t kStreamWS = 8;
   std::vector<std::unique_ptr<StreamWS>> stream_ws;
   bool stream_ws_on = true;
+  uint32_t wsev = 3;  // WG_WSEV (A/B): bit 0 record an event after each use, bit 1 wait on it before the next
 
   int kern = KERN_TRANSPORT;
   // host-API staging
@@ -730,7 +731,7 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
   if (fused && c->stream_ws_on && !(sb->flags & WG_F_UNIFORM) && sb->max_len <= 2048u && c->lpt_one &&
       !(c->lpt_fused && !c->stitch) && slot_plan(c, sb->flags, sb->n, sb->max_len).split > 0) {
     pws = stream_ws(c, s);
-    if (pws && pws->used) HIPTRY(hipStreamWaitEvent(s, pws->ev, 0));
+    if (pws && pws->used && (c->wsev & 2u)) HIPTRY(hipStreamWaitEvent(s, pws->ev, 0));
     // the shared workspace sized too: a later call on a stream being captured into a graph (no workspace of
     // its own, and no allocation possible) plans there
     if (pws && (c->lpt_hist.ensure(2 * wgt::kPlanSet * sizeof(uint32_t)) != WG_OK ||
@@ -842,8 +843,10 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
                                           &c->lpt_order, same_plan);
   }
   if (pws) {  // the workspace's last use, for the next call that takes it
-    if (hipEventRecord(pws->ev, s) != hipSuccess) return fail(WG_EDEVICE, "hipEventRecord failed");
-    pws->used = true;
+    if (c->wsev & 1u) {
+      if (hipEventRecord(pws->ev, s) != hipSuccess) return fail(WG_EDEVICE, "hipEventRecord failed");
+      pws->used = true;
+    }
     return rc;
   }
   const int rr = ordered ? ws_release(c, s) : WG_OK;
@@ -955,6 +958,7 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   if (const char* e = getenv("WG_LPT_FUSED")) c->lpt_fused = atoi(e) != 0;
   if (const char* e = getenv("WG_SLOT2")) c->slot2 = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_STREAM_WS")) c->stream_ws_on = atoi(e) != 0;
+  if (const char* e = getenv("WG_WSEV")) c->wsev = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_FUSED_POLL")) c->fused_poll = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_FUSED_NP")) c->fused_np = (uint32_t)std::max(0, atoi(e));
 #ifdef WG_TEST_HOOKS
