@@ -532,3 +532,46 @@ def test_short_plan_steps_on_destroyed_and_recreated_streams():
             assert np.array_equal(back.cpu().numpy(), want)
     finally:
         eng.close()
+
+
+def test_c2_wide_one_launch_plan_every_packet():
+    """WG_LPT_WIDE=1 (A/B knob, off by default): C2's step planned by ONE k_lpt_one launch over 32 round keys
+    (a sparse longest-first order) and run by k_step<8, 4, ..., kWideBins>, which maps its positions through the
+    counts. Two steps in a row (double-buffered counters): every ct || tag against the oracle, every plaintext
+    back, every status OK."""
+    import os
+    torch, dev = _dev()
+    W = wg()
+    old = os.environ.get("WG_LPT_WIDE")
+    os.environ["WG_LPT_WIDE"] = "1"
+    try:
+        eng = W.Engine(0, key_slots=256)
+    finally:
+        if old is None:
+            del os.environ["WG_LPT_WIDE"]
+        else:
+            os.environ["WG_LPT_WIDE"] = old
+    try:
+        n = 65536
+        lengths, S, off, total, desc = _c2_batch(W, n)
+        keys = splitmix_np(0xC0FFEE, 32 * 256)
+        pt = splitmix_np(0x5EED2030, total)
+        eng.set_keys(0, keys.tobytes())
+        d = torch.from_numpy(W.desc_as_int64(desc)).to(dev)
+        dpt = torch.from_numpy(pt).to(dev)
+        ref = np.zeros(total, np.uint8)
+        O.seal_batch(desc, pt, ref, keys, threads=16)
+        want = pt.copy()
+        for i in range(n):
+            want[int(off[i]) + int(lengths[i]):int(off[i]) + int(S[i])] = 0
+        for _ in range(2):
+            dct = torch.zeros(total, dtype=torch.uint8, device=dev)
+            back = torch.zeros(total, dtype=torch.uint8, device=dev)
+            st = torch.full((n,), 7, dtype=torch.int32, device=dev)
+            eng.duplex(d, dpt, dct, 9000, d, dct, back, st, 9000, uniform=False, after_seal=True)
+            torch.cuda.synchronize()
+            assert np.array_equal(dct.cpu().numpy(), ref)
+            assert int(st.abs().sum().item()) == 0
+            assert np.array_equal(back.cpu().numpy(), want)
+    finally:
+        eng.close()

@@ -132,6 +132,10 @@ struct wg_ctx {
   bool stitch = false;
   // the short-packet split plan's order in one launch (k_lpt_one; WG_LPT_ONE=0: k_lpt_hist + k_lpt_scatter)
   bool lpt_one = true;
+  // ... and for the 8-lane longest-first pairs of other mixed steps (C2; WG_LPT_WIDE=1, A/B): planning 9.9 ->
+  // 6.5 us per C2 step, but k_step 411.8 -> 416.5 us (19 round keys order less finely than the two launches'
+  // 130 bins, and the sparse lookups): C2 -0.3% (profiles/r06_lpt_wide_ab.jsonl); off
+  bool lpt_wide = false;
   // WG_LPT_FUSED=1 (A/B, off): in a k_step_mixed step, planned by the step launch's first workgroups
   // (k_step_mixed_fused) instead of k_lpt_one's own launch. IMIX 66-70 us per step against 59: the planners
   // take 6-8 us while every other workgroup waits, more than the launch gap they remove
@@ -410,7 +414,8 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
                    uint64_t cap_waves, uint32_t G, DevBuf& lpt_hist, DevBuf& lpt_order, wgt::TransportParams* Pout,
                    uint32_t* grid_out, bool* ordered_out, const wgt::RxTables* rx = nullptr,
                    bool private_ws = false, bool reuse_order = false, uint32_t split = 0,
-                   uint32_t* claim = nullptr, uint32_t claim_nc = 0, bool* defer_one = nullptr) {
+                   uint32_t* claim = nullptr, uint32_t claim_nc = 0, bool* defer_one = nullptr,
+                   bool wide_ok = false) {
   bool ordered = false;
   const bool may_defer = defer_one && *defer_one;
   if (defer_one) *defer_one = false;
@@ -485,11 +490,18 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
     // private_ws: buffers owned by the caller's stream (no shared-workspace ordering)
     // one: the short-packet split plan orders in ONE launch (k_lpt_one: sparse order, double-buffered
     // counters, no memset) instead of k_lpt_hist + k_lpt_scatter (WG_LPT_ONE=0: the two launches, A/B)
-    const bool one = mixed && max_len <= 2048u && !claim && c->lpt_one;
+    // wide: the same one-launch plan over up to kWideBins keys for a k_step<8, 4> step of a mixed batch on
+    // the 8-lane longest-first pairs (C2; WG_LPT_WIDE=0: the two launches); wide_ok from launch_after_seal,
+    // and exactly the condition under which it launches k_step<8, 4> (the kernel that reads this order)
+    const uint32_t key_max = (((max_len + 63u) >> 6) + 1u + 7u) >> 3;
+    const bool wide = wide_ok && !mixed && !claim && c->lpt_one && c->lpt_wide && key_max < wgt::kWideBins &&
+                      G == 8 && c->step_wpe4 && 2ull * grid * wgt::TW <= cap_waves && !c->stitch && !c->test_flip;
+    const bool one = (mixed && max_len <= 2048u && !claim && c->lpt_one) || wide;
     if (!reuse_order && one) {
       int rc;
       if ((rc = lpt_hist.ensure(2 * wgt::kPlanSet * sizeof(uint32_t))) != WG_OK) return rc;
-      if ((rc = lpt_order.ensure(sizeof(uint32_t) * wgt::kFastBins * (size_t)n)) != WG_OK) return rc;
+      if ((rc = lpt_order.ensure(sizeof(uint32_t) * (wide ? wgt::kWideBins : wgt::kFastBins) * (size_t)n)) != WG_OK)
+        return rc;
       if (!private_ws && (rc = ws_acquire(c, s)) != WG_OK) return rc;
       if (!lpt_hist.zeroed) {  // a new buffer, or one the two-launch planner wrote histograms into
         HIPTRY(hipMemsetAsync(lpt_hist.p, 0, 2 * wgt::kPlanSet * sizeof(uint32_t), s));
@@ -499,8 +511,12 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
       uint32_t* cnt = (uint32_t*)lpt_hist.p + wgt::kPlanSet * lpt_hist.par;
       uint32_t* nxt = (uint32_t*)lpt_hist.p + wgt::kPlanSet * (lpt_hist.par ^ 1u);
       const uint32_t lgrid = std::max<uint32_t>(1u, std::min<uint32_t>(wgt::LPT_MAX_BLOCKS, (n + 1023u) / 1024u));
-      if (may_defer) {  // the caller's k_step_mixed_fused launch plans (into cnt / nxt, as below)
+      if (may_defer && !wide) {  // the caller's k_step_mixed_fused launch plans (into cnt / nxt, as below)
         *defer_one = true;
+      } else if (wide) {
+        hipLaunchKernelGGL((wgt::k_lpt_one<MODE, wgt::LPT_THREADS, 1, wgt::kWideBins>), dim3(lgrid),
+                           dim3(wgt::LPT_THREADS), 0, s, desc, n, max_len, cnt, nxt, (uint32_t*)lpt_order.p);
+        HIPTRY(hipGetLastError());
       } else {
         // (block shapes of 256 / 512 threads or 4 packets per thread measured the same or slower: 5.0-8.3 us,
         // profiles/r06_lpt_shape_ab.jsonl)
@@ -530,7 +546,7 @@ int plan_transport(wg_ctx* c, const wg_pkt* desc, uint32_t n, const uint8_t* in,
       P.bin_cnt = lpt_hist.last_cnt;
       P.bin_cap = n;
       P.split = split;
-      P.n_long = lpt_hist.last_cnt;  // (marks the launch as mixed)
+      if (mixed) P.n_long = lpt_hist.last_cnt;  // (marks the launch as mixed; a wide plan's k_step is not)
     } else if (mixed) {
       P.n_long = (const uint32_t*)c->lpt_nlong.p;
     }
@@ -770,11 +786,12 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
     rc = plan_transport<WG_MODE_SEAL>(c, sb->desc, sb->n, sb->in, sb->in_size, sb->out, sb->out_size, nullptr,
                                       sb->max_len, sb->flags, s, cap, G, plan_hist, plan_order, &PS, &gs, &os,
                                       nullptr, true, false, sp.split, claim_nc ? (uint32_t*)c->lpt_claim.p : nullptr,
-                                      claim_nc, &defer);
+                                      claim_nc, &defer, true);
     if (rc == WG_OK)
       rc = plan_transport<WG_MODE_OPEN>(c, ob->desc, ob->n, ob->in, ob->in_size, ob->out, ob->out_size, ob->status,
                                         ob->max_len, ob->flags & ~WG_F_AFTER_SEAL, s, cap, G, plan_hist,
-                                        plan_order, &PO, &go, &oo, nullptr, true, true, sp.split);
+                                        plan_order, &PO, &go, &oo, nullptr, true, true, sp.split, nullptr, 0,
+                                        nullptr, true);
     // one issue-priority schedule over the seal and open halves (the rounds of both)
     if (PS.prio_step) PS.prio_step = PO.prio_step = 2u * PS.prio_step;
     if (claim_nc) {
@@ -782,8 +799,12 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
       PO.claim_nc = PS.claim_nc;  // the open half replays the seal's log from the same first positions
       PO.chain_in = (const uint2*)c->lpt_chain.p;
     }
-    if (rc == WG_OK && (gs != go || PS.slots != PO.slots || PS.order != PO.order))
+    if (rc == WG_OK && (gs != go || PS.slots != PO.slots || PS.order != PO.order || PS.bin_cnt != PO.bin_cnt))
       rc = fail(WG_EINVAL, "k_step: seal and open plans differ (%u / %u workgroups)", gs, go);
+    // a sparse (one-launch) order is read only by k_step_mixed* and k_step<8, 4, ..., kWideBins>
+    if (rc == WG_OK && PS.bin_cnt && !PS.n_long && !defer &&
+        !(G == 8 && c->step_wpe4 && 2ull * gs * wgt::TW <= cap && !c->stitch && !c->test_flip && !claim_nc))
+      rc = fail(WG_EINVAL, "k_step: a sparse plan without the kernel that reads it");
 #ifdef WG_DIAG
     if (PO.stamps) PO.stamps += 10ull * gs * wgt::TW;  // the open half's stamps after the seal half's
 #endif
@@ -825,6 +846,9 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
       else if (G == 4) hipLaunchKernelGGL(wgt::k_step<4>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
       else if (c->step_wpe4 && 2ull * gs * wgt::TW <= cap && c->stitch)
         hipLaunchKernelGGL((wgt::k_step<8, WG_STITCH_WPE, false, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
+      else if (c->step_wpe4 && 2ull * gs * wgt::TW <= cap && PS.bin_cnt)  // the wide one-launch plan (sparse order)
+        hipLaunchKernelGGL((wgt::k_step<8, 4, false, false, (int)wgt::kWideBins>), dim3(gs), dim3(64 * wgt::TW), 0, s,
+                           PS, PO, 0u);
       else if (c->step_wpe4 && 2ull * gs * wgt::TW <= cap)
         hipLaunchKernelGGL((wgt::k_step<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
       else if (c->stitch)
@@ -955,6 +979,7 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   if (const char* e = getenv("WG_CLAIM")) c->claim = atoi(e) != 0;
   if (const char* e = getenv("WG_STITCH")) c->stitch = atoi(e) != 0;
   if (const char* e = getenv("WG_LPT_ONE")) c->lpt_one = atoi(e) != 0;
+  if (const char* e = getenv("WG_LPT_WIDE")) c->lpt_wide = atoi(e) != 0;
   if (const char* e = getenv("WG_LPT_FUSED")) c->lpt_fused = atoi(e) != 0;
   if (const char* e = getenv("WG_SLOT2")) c->slot2 = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_STREAM_WS")) c->stream_ws_on = atoi(e) != 0;

@@ -322,6 +322,9 @@ __device__ __forceinline__ uint32_t batch_pos(uint32_t g, uint32_t k, uint32_t S
 // batch position -> packet index: the identity, the dense longest-first order, or the sparse one of k_lpt_one
 // (keys descending, key k's packets at order[k * bin_cap + i])
 constexpr uint32_t kFastBins = 6;  // keys 0..5: every packet of at most 2,048 B (33 blocks, 5 rounds of 8)
+// the same one-launch plan for other mixed batches whose keys fit 32 bins (max_len <= 15,808 B: C2's 9,000-B
+// packets are key 18), read by k_step<8, 4, ..., kWideBins>
+constexpr uint32_t kWideBins = 32;
 // k_lpt_one's per-key counters, kCntStride words apart (every planner workgroup adds to each once). 16 (a
 // 64-B line each) measured the same as 1: the planner's 5.1 us is not atomic contention
 // (profiles/r06_cnt_stride_ab.jsonl)
@@ -329,7 +332,7 @@ constexpr uint32_t kFastBins = 6;  // keys 0..5: every packet of at most 2,048 B
 #define WG_CNT_STRIDE 1
 #endif
 constexpr uint32_t kCntStride = WG_CNT_STRIDE;
-template <bool MX>
+template <int MX>  // MX: bins of the sparse order (kFastBins for the short-packet plan, kWideBins), 0: dense
 __device__ __forceinline__ uint32_t pkt_at(const TransportParams& P, uint32_t pos) {
   if (MX && P.bin_cap) {
     // the counts through the scalar cache (constant for the launch), not held in SGPRs across the body
@@ -338,7 +341,7 @@ __device__ __forceinline__ uint32_t pkt_at(const TransportParams& P, uint32_t po
     const uint32_t p = P.pos_base + pos;
     uint32_t start = 0, at = 0;
 #pragma unroll
-    for (int k = (int)kFastBins - 1; k >= 0; --k) {
+    for (int k = MX - 1; k >= 0; --k) {
       const uint32_t c = bc[k * kCntStride];
       at = (p >= start) ? (uint32_t)k * P.bin_cap + (p - start) : at;
       start += c;
@@ -390,7 +393,7 @@ constexpr int kPosStatic = 0, kPosClaim = 1, kPosChain = 2;
 // issued after them, so the image still holds the round's MAC input while they read it. A packet's last
 // round takes its Horner steps after its XOR phase as before (nothing follows it to hide them in).
 // MX: the launch is a k_*_mixed part (its positions may map through k_lpt_one's sparse order)
-template <int MODE, int G = 8, bool VF = false, int PM = kPosStatic, bool ST = false, bool MX = false>
+template <int MODE, int G = 8, bool VF = false, int PM = kPosStatic, bool ST = false, int MX = 0>
 __device__ __forceinline__ void transport_body(const TransportParams& P, uint32_t blk, uint32_t wv, uint4* const img,
                                                SlotRec* const rec, uint32_t& iter) {
   static_assert(MODE == WG_MODE_SEAL || MODE == WG_MODE_OPEN, "transport modes only");
@@ -1030,8 +1033,8 @@ __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(8)
   TransportParams Q;
   uint32_t qb = 0, iter = 0;
   const int g = mixed_part<GS>(P, blockIdx.x, Q, qb);
-  if (g == 16) transport_body<MODE, 16, VF, kPosStatic, false, true>(Q, qb, wv, img_[wv], rec_[wv], iter);
-  else if (g == GS) transport_body<MODE, GS, VF, kPosStatic, false, true>(Q, qb, wv, img_[wv], rec_[wv], iter);
+  if (g == 16) transport_body<MODE, 16, VF, kPosStatic, false, (int)kFastBins>(Q, qb, wv, img_[wv], rec_[wv], iter);
+  else if (g == GS) transport_body<MODE, GS, VF, kPosStatic, false, (int)kFastBins>(Q, qb, wv, img_[wv], rec_[wv], iter);
 }
 
 #ifndef WG_STITCH_WPE
@@ -1053,18 +1056,18 @@ k_step_mixed(TransportParams S, TransportParams O) {
   const int g = mixed_part<GS, GT>(S, blockIdx.x, QS, qb);
   (void)mixed_part<GS, GT>(O, blockIdx.x, QO, qb2);  // the same split: the open batch has the seal's lengths
   if (g == 16) {
-    transport_body<WG_MODE_SEAL, 16, false, kPosStatic, ST, true>(QS, qb, wv, img_[wv], rec, iter);
+    transport_body<WG_MODE_SEAL, 16, false, kPosStatic, ST, (int)kFastBins>(QS, qb, wv, img_[wv], rec, iter);
     asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
-    transport_body<WG_MODE_OPEN, 16, false, kPosStatic, ST, true>(QO, qb, wv, img_[wv], rec, iter);
+    transport_body<WG_MODE_OPEN, 16, false, kPosStatic, ST, (int)kFastBins>(QO, qb, wv, img_[wv], rec, iter);
   } else if (g == GS) {
-    transport_body<WG_MODE_SEAL, GS, false, kPosStatic, ST, true>(QS, qb, wv, img_[wv], rec, iter);
+    transport_body<WG_MODE_SEAL, GS, false, kPosStatic, ST, (int)kFastBins>(QS, qb, wv, img_[wv], rec, iter);
     asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
-    transport_body<WG_MODE_OPEN, GS, false, kPosStatic, ST, true>(QO, qb, wv, img_[wv], rec, iter);
+    transport_body<WG_MODE_OPEN, GS, false, kPosStatic, ST, (int)kFastBins>(QO, qb, wv, img_[wv], rec, iter);
   } else if constexpr (GT != 0) {
     if (g == GT) {
-      transport_body<WG_MODE_SEAL, GT, false, kPosStatic, false, true>(QS, qb, wv, img_[wv], rec, iter);
+      transport_body<WG_MODE_SEAL, GT, false, kPosStatic, false, (int)kFastBins>(QS, qb, wv, img_[wv], rec, iter);
       asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
-      transport_body<WG_MODE_OPEN, GT, false, kPosStatic, false, true>(QO, qb, wv, img_[wv], rec, iter);
+      transport_body<WG_MODE_OPEN, GT, false, kPosStatic, false, (int)kFastBins>(QO, qb, wv, img_[wv], rec, iter);
     }
   }
 }
@@ -1126,19 +1129,19 @@ __device__ __forceinline__ void step_test_flip(const TransportParams& S, uint32_
 
 // FLIP: the test-hook instantiation (WG_TEST_STEP_FLIP), launched only by the test library (WG_TEST_HOOKS);
 // the product instantiations carry no hook code at all.
-template <int G = 8, int WPE = 8, bool FLIP = false, bool ST = false>
+template <int G = 8, int WPE = 8, bool FLIP = false, bool ST = false, int MX = 0>
 __global__ void __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_step(TransportParams S, TransportParams O, uint32_t test_flip) {
   __shared__ uint4 img_[TW][4 * 64];
   __shared__ SlotRec rec_[TW][64 / G < 8 ? 8 : 64 / G];
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t iter = 0;  // one issue-priority schedule over both halves (plan_transport: prio_step of the step)
-  transport_body<WG_MODE_SEAL, G, false, kPosStatic, ST>(S, blockIdx.x, wv, img_[wv], rec_[wv], iter);
+  transport_body<WG_MODE_SEAL, G, false, kPosStatic, ST, MX>(S, blockIdx.x, wv, img_[wv], rec_[wv], iter);
   // the open reads the ciphertext and tags this wave just stored: wait until the stores are
   // performed and drop this CU's L1 lines (an in-place seal read the plaintext through them)
   asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
   if constexpr (FLIP) step_test_flip<G>(S, blockIdx.x, wv, test_flip);
-  transport_body<WG_MODE_OPEN, G, false, kPosStatic, ST>(O, blockIdx.x, wv, img_[wv], rec_[wv], iter);
+  transport_body<WG_MODE_OPEN, G, false, kPosStatic, ST, MX>(O, blockIdx.x, wv, img_[wv], rec_[wv], iter);
 }
 
 // k_step with dynamic claims (mixed-length batches, WG_CLAIM): the seal half claims its slots' packets
@@ -1259,20 +1262,20 @@ __global__ void __launch_bounds__(LPT_THREADS) k_lpt_scatter(const wg_pkt* d, ui
 
 // k_lpt_one's counter set per call: the counts kCntStride words apart, the fused step's publication count at
 // kPlanDone), two sets used in turn
-constexpr uint32_t kPlanDone = kFastBins * kCntStride > 32u ? kFastBins * kCntStride : 32u;
+constexpr uint32_t kPlanDone = kWideBins * kCntStride > 32u ? kWideBins * kCntStride : 32u;
 constexpr uint32_t kPlanSet = kPlanDone + 32u;  // words per set (the publication count on a line of its own)
 
-// The body of k_lpt_one for block `blk` of `nblk` with `threads` threads: h / base are kFastBins words of LDS.
+// The body of k_lpt_one for block `blk` of `nblk` with `threads` threads over NB keys: h / base are NB words of LDS.
 // A thread takes KPT packets per trip, their descriptor loads issued together, and when the block's range is
 // one trip (the usual case) keeps the keys for the scatter pass: two load latencies per plan, not 2 x trips.
-template <int MODE, int KPT = 1>
+template <int MODE, int KPT = 1, uint32_t NB = kFastBins>
 __device__ __forceinline__ void lpt_one_body(const wg_pkt* d, uint32_t n, uint32_t max_len, uint32_t* cnt,
                                              uint32_t* cnt_next, uint32_t* order, uint32_t blk, uint32_t nblk,
                                              uint32_t threads, uint32_t* h, uint32_t* base) {
-  if (threadIdx.x < kFastBins) h[threadIdx.x] = 0;
-  // the next call's counts ([0, kFastBins)) and k_step_mixed_fused's publication count (kPlanDone: its own line,
+  if (threadIdx.x < NB) h[threadIdx.x] = 0;
+  // the next call's counts ([0, NB)) and k_step_mixed_fused's publication count (kPlanDone: its own line,
   // away from the counts' atomics)
-  if (blk == 0 && ((threadIdx.x < kFastBins * kCntStride && threadIdx.x % kCntStride == 0u) || threadIdx.x == kPlanDone))
+  if (blk == 0 && ((threadIdx.x < kWideBins * kCntStride && threadIdx.x % kCntStride == 0u) || threadIdx.x == kPlanDone))
     cnt_next[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t per = (n + nblk - 1u) / nblk;
@@ -1285,21 +1288,21 @@ __device__ __forceinline__ void lpt_one_body(const wg_pkt* d, uint32_t n, uint32
     uint64_t mine = 0;
     uint32_t cnt_k = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < kFastBins; ++k) {
+    for (uint32_t k = 0; k < NB; ++k) {
       const uint64_t m = __ballot(key == k);
       mine = key == k ? m : mine;
       cnt_k = lane == k ? (uint32_t)__popcll(m) : cnt_k;
     }
     uint32_t b = 0;
-    if (cnt_k) b = atomicAdd(&slots[lane], cnt_k);  // lanes 0..kFastBins-1 only (cnt_k = 0 elsewhere)
-    b = __shfl(b, (int)(key < kFastBins ? key : 0u), 64);
+    if (cnt_k) b = atomicAdd(&slots[lane], cnt_k);  // lanes 0..NB-1 only (cnt_k = 0 elsewhere)
+    b = __shfl(b, (int)(key < NB ? key : 0u), 64);
     return b + (uint32_t)__popcll(mine & ((1ull << lane) - 1ull));
   };
   auto keys_at = [&](uint32_t i0, uint32_t (&key)[KPT]) {  // every lane of a wave takes part in each trip
 #pragma unroll
     for (int t = 0; t < KPT; ++t) {
       const uint32_t i = i0 + t * threads + threadIdx.x;
-      key[t] = i < hi ? lpt_key<MODE>(d, i, max_len) : kFastBins;
+      key[t] = i < hi ? lpt_key<MODE>(d, i, max_len) : NB;
     }
   };
   uint32_t key[KPT];
@@ -1309,7 +1312,7 @@ __device__ __forceinline__ void lpt_one_body(const wg_pkt* d, uint32_t n, uint32
     for (int t = 0; t < KPT; ++t) (void)wave_rank(h, key[t]);
   }
   __syncthreads();
-  if (threadIdx.x < kFastBins) {
+  if (threadIdx.x < NB) {
     const uint32_t k = threadIdx.x, c = h[k];
     base[k] = k * n + (c ? atomicAdd(&cnt[k * kCntStride], c) : 0u);
   }
@@ -1333,11 +1336,11 @@ __device__ __forceinline__ void lpt_one_body(const wg_pkt* d, uint32_t n, uint32
 // The counters are double-buffered by call (cnt for this call, zero on entry; cnt_next zeroed here for the
 // next), so no memset launch either. Order inside a key: arbitrary (every position of the order is a packet).
 // (THREADS, KPT: the block shape)
-template <int MODE, uint32_t THREADS = LPT_THREADS, int KPT = 1>
+template <int MODE, uint32_t THREADS = LPT_THREADS, int KPT = 1, uint32_t NB = kFastBins>
 __global__ void __launch_bounds__(THREADS) k_lpt_one(const wg_pkt* d, uint32_t n, uint32_t max_len, uint32_t* cnt,
                                                      uint32_t* cnt_next, uint32_t* order) {
-  __shared__ uint32_t h[kFastBins], base[kFastBins];
-  lpt_one_body<MODE, KPT>(d, n, max_len, cnt, cnt_next, order, blockIdx.x, gridDim.x, THREADS, h, base);
+  __shared__ uint32_t h[NB], base[NB];
+  lpt_one_body<MODE, KPT, NB>(d, n, max_len, cnt, cnt_next, order, blockIdx.x, gridDim.x, THREADS, h, base);
 }
 
 // k_step_mixed with its planning folded in (WG_LPT_FUSED, the short-packet plan): workgroups [0, np) plan as
@@ -1417,13 +1420,13 @@ k_step_mixed_fused(TransportParams S, TransportParams O, uint32_t np, uint32_t* 
   const int g = mixed_part<GS>(S, blk, QS, qb);
   (void)mixed_part<GS>(O, blk, QO, qb2);
   if (g == 16) {
-    transport_body<WG_MODE_SEAL, 16, false, kPosStatic, ST, true>(QS, qb, wv, img_[wv], rec_[wv], iter);
+    transport_body<WG_MODE_SEAL, 16, false, kPosStatic, ST, (int)kFastBins>(QS, qb, wv, img_[wv], rec_[wv], iter);
     asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
-    transport_body<WG_MODE_OPEN, 16, false, kPosStatic, ST, true>(QO, qb, wv, img_[wv], rec_[wv], iter);
+    transport_body<WG_MODE_OPEN, 16, false, kPosStatic, ST, (int)kFastBins>(QO, qb, wv, img_[wv], rec_[wv], iter);
   } else if (g == GS) {
-    transport_body<WG_MODE_SEAL, GS, false, kPosStatic, ST, true>(QS, qb, wv, img_[wv], rec_[wv], iter);
+    transport_body<WG_MODE_SEAL, GS, false, kPosStatic, ST, (int)kFastBins>(QS, qb, wv, img_[wv], rec_[wv], iter);
     asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0" ::: "memory");
-    transport_body<WG_MODE_OPEN, GS, false, kPosStatic, ST, true>(QO, qb, wv, img_[wv], rec_[wv], iter);
+    transport_body<WG_MODE_OPEN, GS, false, kPosStatic, ST, (int)kFastBins>(QO, qb, wv, img_[wv], rec_[wv], iter);
   }
   WG_FUSED_STAMP(2, __builtin_amdgcn_s_memrealtime());
 }
