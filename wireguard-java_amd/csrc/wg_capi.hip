@@ -6,6 +6,7 @@
 // on-device self test. No CPU crypto lives here: every seal/open/cipher/MAC runs in
 // a HIP kernel, and every entry point fails with WG_EDEVICE when no HIP device is usable.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <hipcub/hipcub.hpp>
 #include <linux/futex.h>
 #include <pthread.h>
@@ -170,6 +171,7 @@ struct wg_ctx {
   static constexpr size_t kStreamWS = 8;
   std::vector<std::unique_ptr<StreamWS>> stream_ws;
   bool stream_ws_on = true;
+  bool ws_ext = true;  // WG_WS_EXT=0: the workspace event as a hipEventRecord after the step launch (A/B)
   uint32_t wsev = 3;  // WG_WSEV (A/B): bit 0 record an event after each use, bit 1 wait on it before the next
 
   int kern = KERN_TRANSPORT;
@@ -754,6 +756,7 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
                 c->lpt_order.ensure(sizeof(uint32_t) * wgt::kFastBins * (size_t)sb->n) != WG_OK))
       return WG_ENOMEM;
   }
+  hipEvent_t stop_ev = nullptr;  // set when the step kernel's launch records the workspace event itself
   DevBuf& plan_hist = pws ? pws->hist : c->lpt_hist;
   DevBuf& plan_order = pws ? pws->order : c->lpt_order;
   if (ordered && !pws && (rc = ws_acquire(c, s)) != WG_OK) return rc;
@@ -811,6 +814,14 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
     if (rc == WG_OK) {
       hipEvent_t ev;
       record_start(c, s, &ev);
+      // the workspace's last-use event rides on the step kernel's own completion signal (hipExtLaunchKernel's
+      // stop event): a separate hipEventRecord after the launch costs a 3-us gap between steps (IMIX 6%,
+      // profiles/r06_ws_event_ab.jsonl). Not while the stream is being captured into a graph.
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (c->ws_ext && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone && !ev)
+        stop_ev = pws ? pws->ev : (ordered ? c->ev_ws : nullptr);
+#define WG_XLAUNCH(kern, grid, block, shm, strm, ...) \
+  hipExtLaunchKernelGGL(kern, grid, block, shm, strm, nullptr, stop_ev, 0u, __VA_ARGS__)
       if (defer) {  // the planner's blocks first (as k_lpt_one's grid, with 64 x TW threads each), then the step's
         uint32_t np = std::max<uint32_t>(1u, std::min<uint32_t>(wgt::LPT_MAX_BLOCKS, (sb->n + 1023u) / 1024u));
         if (c->fused_np) np = std::min<uint32_t>(c->fused_np, std::max<uint32_t>(1u, sb->n / 256u));
@@ -819,41 +830,42 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
         uint32_t* err = nullptr;
         HIPTRY(hipHostGetDevicePointer((void**)&err, c->plan_err, 0));
         if (sp.gs == 4)
-          hipLaunchKernelGGL(wgt::k_step_mixed_fused<4>, dim3(np + gs), dim3(64 * wgt::TW), 0, s, PS, PO, np, cnt, nxt, err,
+          WG_XLAUNCH(wgt::k_step_mixed_fused<4>, dim3(np + gs), dim3(64 * wgt::TW), 0, s, PS, PO, np, cnt, nxt, err,
                              c->fused_poll);
         else
-          hipLaunchKernelGGL(wgt::k_step_mixed_fused<8>, dim3(np + gs), dim3(64 * wgt::TW), 0, s, PS, PO, np, cnt, nxt, err,
+          WG_XLAUNCH(wgt::k_step_mixed_fused<8>, dim3(np + gs), dim3(64 * wgt::TW), 0, s, PS, PO, np, cnt, nxt, err,
                              c->fused_poll);
-      } else if (claim_nc) hipLaunchKernelGGL((wgt::k_step_claim<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+      } else if (claim_nc) WG_XLAUNCH((wgt::k_step_claim<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else if (PS.n_long && sp.gs == 4 && c->stitch)
-        hipLaunchKernelGGL((wgt::k_step_mixed<4, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+        WG_XLAUNCH((wgt::k_step_mixed<4, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else if (PS.n_long && sp.gs == 4 && PS.bin_cnt && c->slot2 && c->slot2 < sp.split && c->key_slots < (1u << 24)) {
         PS.split2 = PO.split2 = c->slot2;  // a third part: the grid's upper bound grows by one workgroup
-        hipLaunchKernelGGL((wgt::k_step_mixed<4, false, 2>), dim3(gs + 1), dim3(64 * wgt::TW), 0, s, PS, PO);
-      } else if (PS.n_long && sp.gs == 4) hipLaunchKernelGGL(wgt::k_step_mixed<4>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+        WG_XLAUNCH((wgt::k_step_mixed<4, false, 2>), dim3(gs + 1), dim3(64 * wgt::TW), 0, s, PS, PO);
+      } else if (PS.n_long && sp.gs == 4) WG_XLAUNCH(wgt::k_step_mixed<4>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
       else if (PS.n_long && c->stitch)
-        hipLaunchKernelGGL((wgt::k_step_mixed<8, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
-      else if (PS.n_long) hipLaunchKernelGGL(wgt::k_step_mixed<8>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+        WG_XLAUNCH((wgt::k_step_mixed<8, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
+      else if (PS.n_long) WG_XLAUNCH(wgt::k_step_mixed<8>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO);
 #ifdef WG_TEST_HOOKS
       else if (c->test_flip && G == 8)  // test hook build: the same body with the tag flip between the halves
-        hipLaunchKernelGGL((wgt::k_step<8, 4, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, c->test_flip);
+        WG_XLAUNCH((wgt::k_step<8, 4, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, c->test_flip);
 #endif
       else if (G == 16 && c->stitch)
-        hipLaunchKernelGGL((wgt::k_step<16, WG_STITCH_WPE, false, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
-      else if (G == 16) hipLaunchKernelGGL(wgt::k_step<16>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
+        WG_XLAUNCH((wgt::k_step<16, WG_STITCH_WPE, false, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
+      else if (G == 16) WG_XLAUNCH(wgt::k_step<16>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
       else if (G == 4 && c->stitch)
-        hipLaunchKernelGGL((wgt::k_step<4, WG_STITCH_WPE, false, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
-      else if (G == 4) hipLaunchKernelGGL(wgt::k_step<4>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
+        WG_XLAUNCH((wgt::k_step<4, WG_STITCH_WPE, false, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
+      else if (G == 4) WG_XLAUNCH(wgt::k_step<4>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
       else if (c->step_wpe4 && 2ull * gs * wgt::TW <= cap && c->stitch)
-        hipLaunchKernelGGL((wgt::k_step<8, WG_STITCH_WPE, false, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
+        WG_XLAUNCH((wgt::k_step<8, WG_STITCH_WPE, false, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
       else if (c->step_wpe4 && 2ull * gs * wgt::TW <= cap && PS.bin_cnt)  // the wide one-launch plan (sparse order)
-        hipLaunchKernelGGL((wgt::k_step<8, 4, false, false, (int)wgt::kWideBins>), dim3(gs), dim3(64 * wgt::TW), 0, s,
+        WG_XLAUNCH((wgt::k_step<8, 4, false, false, (int)wgt::kWideBins>), dim3(gs), dim3(64 * wgt::TW), 0, s,
                            PS, PO, 0u);
       else if (c->step_wpe4 && 2ull * gs * wgt::TW <= cap)
-        hipLaunchKernelGGL((wgt::k_step<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
+        WG_XLAUNCH((wgt::k_step<8, 4>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
       else if (c->stitch)
-        hipLaunchKernelGGL((wgt::k_step<8, WG_STITCH_WPE, false, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
-      else hipLaunchKernelGGL(wgt::k_step<8>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
+        WG_XLAUNCH((wgt::k_step<8, WG_STITCH_WPE, false, true>), dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
+      else WG_XLAUNCH(wgt::k_step<8>, dim3(gs), dim3(64 * wgt::TW), 0, s, PS, PO, 0u);
+#undef WG_XLAUNCH
       const hipError_t e = hipGetLastError();
       record_end(c, s, ev);
       if (e != hipSuccess) rc = fail(WG_EDEVICE, "k_step launch: %s", hipGetErrorString(e));
@@ -867,10 +879,16 @@ int launch_after_seal(wg_ctx* c, const wg_batch* sb, const wg_batch* ob, hipStre
                                           &c->lpt_order, same_plan);
   }
   if (pws) {  // the workspace's last use, for the next call that takes it
-    if (c->wsev & 1u) {
+    if (stop_ev && rc == WG_OK) {
+      pws->used = true;
+    } else if (c->wsev & 1u) {
       if (hipEventRecord(pws->ev, s) != hipSuccess) return fail(WG_EDEVICE, "hipEventRecord failed");
       pws->used = true;
     }
+    return rc;
+  }
+  if (ordered && stop_ev && rc == WG_OK) {  // ws_release's record done by the step kernel's completion
+    c->ws_stream = s;
     return rc;
   }
   const int rr = ordered ? ws_release(c, s) : WG_OK;
@@ -984,6 +1002,7 @@ int wg_ctx_create(int device, uint32_t key_slots, wg_ctx** out) {
   if (const char* e = getenv("WG_SLOT2")) c->slot2 = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_STREAM_WS")) c->stream_ws_on = atoi(e) != 0;
   if (const char* e = getenv("WG_WSEV")) c->wsev = (uint32_t)std::max(0, atoi(e));
+  if (const char* e = getenv("WG_WS_EXT")) c->ws_ext = atoi(e) != 0;
   if (const char* e = getenv("WG_FUSED_POLL")) c->fused_poll = (uint32_t)std::max(0, atoi(e));
   if (const char* e = getenv("WG_FUSED_NP")) c->fused_np = (uint32_t)std::max(0, atoi(e));
 #ifdef WG_TEST_HOOKS
