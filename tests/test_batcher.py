@@ -315,14 +315,13 @@ def test_held_caller_delays_nobody():
     assert j["held_us"] >= 50000
     assert j["lat_us"]["p999"] < 2000, j["lat_us"]
     # The single slowest of the 32,000 calls, with its stages (wg_pp_last_call) and the caller thread's
-    # context switches: the device served it in its usual ~8 us, and it stayed under 2 ms unless the OS
-    # preempted the calling thread during it (an involuntary context switch: round 5 traced every
-    # 0.2-ms outlier of six runs to one) or the cgroup quota throttled the process.
-    # Waiting for the held entry would add 50 ms.
+    # context switches. Waiting for the held entry would add 50 ms, so the slowest call must stay far
+    # below that. It usually stays under 2 ms (the device serves a call in ~8 us; round 5 traced every
+    # 0.2-ms outlier to an OS preemption of the caller), but one round-6 box stalled the
+    # device itself for 3.75 ms under 16 concurrent calls (device_service_us 3754.8, no preemption, no
+    # throttling): a device-wide pause, not a wait for the held entry, so the bound is 10 ms.
     slow = j["slowest"]
-    assert slow["device_service_us"] < 100, slow
-    preempted = slow["involuntary_csw"] > 0 or j["throttled_periods"] > 0
-    assert j["lat_us"]["max"] < (20000 if preempted else 2000), (j["lat_us"], slow, j["throttled_periods"])
+    assert j["lat_us"]["max"] < 10000, (j["lat_us"], slow, j["throttled_periods"])
 
 
 @pytest.mark.gpu
